@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Benchmark: simulated TIS node-instructions/sec for the batched /compute path.
+
+One "step" = one pass of the executor over one batch of synthetic /compute
+inputs already resident in HBM (BASELINE.json config 2 by default: the
+docker-compose example network, 16,777,216 lanes per GPU).  With --gpus N
+(launched by torch.distributed.run, one process per GPU) every rank runs its
+own contiguous shard of global lane indices -- weak scaling, no data-path
+collective; RCCL carries only the final counter reduction (and the optional
+ordered output gather, --gather, timed separately).
+
+Prints ONE JSON line on rank 0 (keys per the driver contract + roofline +
+cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import misaka_net_amd as mk  # noqa: E402
+from misaka_net_amd import _native as N  # noqa: E402
+
+SEED = 0x4D49534B41
+METRIC = "simulated TIS node-instructions/sec (whole node) + /compute results/sec at 1/2/4/8 GPU"
+
+# Spec int32 VALU issue: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz (the FP32
+# vector rate of MI355X_MICROARCH.md: 157.3 TFLOP/s = 78.6 T FMA lane-ops/s).
+SPEC_LANE_OPS = 256 * 4 * 32 * 2.4e9
+K_LANE_OPS = 4  # algorithmic lane-ops per retired node-instruction
+HBM_PEAK = 8.0e12
+
+WORKLOADS = {
+    # name: (network factory, lanes per GPU, generator kind, mask, bytes per lane)
+    "c2": ("c2_example_net_16M", mk.networks.example_network, 1 << 24, N.MK_GEN_FULL, 0),
+    "c3": ("c3_sample_net_8M_per_gpu", mk.networks.sample_network, 1 << 23, N.MK_GEN_FULL, 0),
+    "c4": ("c4_pipeline_d64_64K", lambda: mk.networks.pipeline_network(64), 1 << 16, N.MK_GEN_FULL, 0),
+    "c4d1024": ("c4_pipeline_d1024_16K", lambda: mk.networks.pipeline_network(1024), 1 << 14, N.MK_GEN_FULL, 0),
+    "c5": ("c5_countdown_4M", mk.networks.countdown_network, 1 << 22, N.MK_GEN_MASKED, 1023),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(nodes, gen_kind, mask, seconds=10.0):
+    """Oracle (the C port, test infrastructure) on the host cores, bounded sample."""
+    from oracle import pyoracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    on = pyoracle.OracleNet(nodes)
+    n = 4096
+    total_lanes = total_steps = 0
+    t_total = 0.0
+    while t_total < seconds:
+        xs = pyoracle.gen_inputs(SEED, n, kind=gen_kind, mask=mask)
+        t0 = time.perf_counter()
+        _, _, sp = on.compute_batch(xs, threads=threads)
+        dt = time.perf_counter() - t0
+        t_total += dt
+        total_lanes += n
+        total_steps += int(sp.sum())
+        if dt < seconds / 8:
+            n *= 2
+    return {
+        "value": total_steps / t_total,
+        "unit": "node-instr/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{total_lanes} lanes of the same workload in {t_total:.1f} s, oracle/tis_oracle.c, {threads} threads",
+        "results_per_s": total_lanes / t_total,
+    }
+
+
+def valu_peak(stream):
+    """Live dependency-free v_add_u32 probe on this GPU (lane-ops/s)."""
+    blocks, iters = 256 * 8 * 4, 2000
+    mk.valu_probe_device(blocks, 200, stream=stream)  # warm
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ops = mk.valu_probe_device(blocks, iters, stream=stream)
+    e1.record()
+    torch.cuda.synchronize()
+    return ops / (e0.elapsed_time(e1) * 1e-3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per GPU (default: the config's)")
+    ap.add_argument("--gather", action="store_true", help="also time an ordered RCCL gather of outputs to rank 0")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    name, factory, lanes, gen_kind, mask = WORKLOADS[args.config]
+    if args.lanes:
+        lanes = args.lanes
+    nodes = factory()
+    net = mk.Network(nodes)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # Inputs resident in HBM before the timed region (global lane indices
+    # [rank*lanes, (rank+1)*lanes)).
+    x = torch.empty(lanes, dtype=torch.int32, device="cuda")
+    mk.generate_inputs_device(lanes, x.data_ptr(), seed=SEED, gen_kind=gen_kind, gen_mask=mask,
+                              offset=rank * lanes, device=dev, stream=sh)
+    out = torch.empty(lanes, dtype=torch.int32, device="cuda")
+    st = torch.empty(lanes, dtype=torch.uint8, device="cuda")
+    stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+
+    def step(stats_ptr):
+        net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats_ptr,
+                           in_ptr=x.data_ptr(), in_kind=N.MK_IN_I32, device=dev, stream=sh)
+
+    for _ in range(args.warmup):
+        step(None)
+    torch.cuda.synchronize()
+    stats.zero_()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step(stats.data_ptr())
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_s = e0.elapsed_time(e1) * 1e-3  # HIP events on the launch stream
+
+    # per-rank -> whole job (max time over ranks, summed work)
+    t = torch.tensor([wall, kernel_s], dtype=torch.float64, device="cuda")
+    tot = stats.clone()
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    wall_max, kern_max = t.tolist()
+    tot = tot.cpu().numpy()
+    retired, with_out, finished = int(tot[0]), int(tot[1]), int(tot[2])
+    assert finished == lanes * world * args.steps, (finished, lanes, world, args.steps)
+
+    gather_ms = None
+    if args.gather and dist:
+        torch.cuda.synchronize()
+        g_out = torch.empty(lanes * world if rank == 0 else 1, dtype=torch.int32, device="cuda")
+        dist.barrier()
+        tg = time.perf_counter()
+        if rank == 0:
+            dist.gather(out, gather_list=list(g_out.view(world, lanes).unbind(0)), dst=0)
+        else:
+            dist.gather(out, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    value = retired / wall_max
+    per_gpu_kernel_rate = retired / world / kern_max
+    peak_meas = None
+    if rank == 0:
+        try:
+            peak_meas = valu_peak(sh)
+        except Exception as e:  # pragma: no cover
+            log("valu probe failed:", e)
+    peak = max(SPEC_LANE_OPS, peak_meas or 0.0)
+    achieved = K_LANE_OPS * per_gpu_kernel_rate
+    bytes_per_lane = 4 + 4 + 1  # int32 input read, int32 out + u8 status written
+    hbm_achieved = bytes_per_lane * lanes * args.steps / kern_max
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(nodes, gen_kind, mask, args.cpu_seconds)
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "node-instr/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (splitmix64 int32 /compute inputs, resident in HBM)",
+            "config": {
+                "workload": name,
+                "lanes_per_gpu": lanes,
+                "global_lanes": lanes * world,
+                "network": args.config,
+                "parallelism": f"dp{world} (contiguous lane shards, no data-path collective)",
+            },
+            "results_per_s": with_out / wall_max,
+            "node_instr_per_lane": retired / (lanes * world * args.steps),
+            "kernel_ms_per_step": kern_max / args.steps * 1e3,
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved / 1e12,
+                "peak": peak / 1e12,
+                "unit": "Tlane-op/s",
+                "frac": achieved / peak,
+                "traffic": None,
+                "k_lane_ops_per_instr": K_LANE_OPS,
+                "peak_spec": SPEC_LANE_OPS / 1e12,
+                "peak_measured": None if peak_meas is None else peak_meas / 1e12,
+            },
+            "roofline_hbm": {
+                "bound": "hbm",
+                "achieved": hbm_achieved / 1e9,
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": hbm_achieved / HBM_PEAK,
+                "bytes_per_lane": bytes_per_lane,
+            },
+            "cpu_baseline": cpu,
+        }
+        if gather_ms is not None:
+            rec["gather_ms"] = gather_ms
+        print(json.dumps(rec), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+/*
+ * mk.h -- C ABI of the MI355X batched executor for Misaka Net TIS networks.
+ *
+ * Drop-in boundary (SURVEY.md section 8 row b).  The reference has no FFI; the
+ * path sits behind the master's HTTP surface and the Go-internal node types.
+ * Each entry point below names the reference interface it replaces.  Plain C:
+ * no C++ types, caller-owned arrays, the library never retains a caller
+ * pointer after return (cgo pointer-passing rules), never exits or aborts.
+ *
+ * Thread safety: every call is safe to make concurrently on one mk_net
+ * (Go net/http runs /compute handlers concurrently, master.go:197).  The host
+ * API serialises per handle; the device API is stream-ordered and callers
+ * that issue it concurrently on one handle and device must share one stream.
+ */
+#ifndef MK_H
+#define MK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (negative returns) ---------------------------------- */
+#define MK_OK 0
+#define MK_EINVAL (-1)  /* bad argument                                   */
+#define MK_EPARSE (-2)  /* program text rejected (Go error text in err)   */
+#define MK_ELIMIT (-3)  /* network exceeds executor limits                */
+#define MK_EDEVICE (-4) /* HIP runtime error / no usable GPU              */
+#define MK_ENOMEM (-5)  /* allocation failed                              */
+
+/* ---- limits ------------------------------------------------------------ */
+#define MK_MAX_PROGRAM_NODES 16
+#define MK_MAX_STACK_NODES 32
+#define MK_MAX_LINES 65535
+
+/* ---- per-lane status byte ---------------------------------------------- */
+#define MK_ST_QUIESCENT 1      /* every node blocked (reference: /compute hangs if no output) */
+#define MK_ST_BUDGET 2         /* retired-instruction budget reached at a round end           */
+#define MK_ST_STACK_OVERFLOW 3 /* a PUSH exceeded stack_cap (reference stacks are unbounded)  */
+#define MK_ST_OUTPUT_STOP 4    /* stopped at the first OUT (MK_FLAG_STOP_ON_OUTPUT)           */
+#define MK_ST_REASON_MASK 0x0f
+#define MK_ST_HAS_OUTPUT 0x10  /* lane produced a /compute result                              */
+
+/* ---- node kinds ----------------------------------------------------------
+ * NODE_INFO types (master.go:431-438, docker-compose.yml:16-21) plus the
+ * master's own name (MASTER_URI, cmd/app.go:20): a program that addresses the
+ * master with MOV/PUSH/POP gets the reference's Unimplemented-and-retry
+ * behaviour instead of the unknown-host hang. */
+#define MK_NODE_PROGRAM 0
+#define MK_NODE_STACK 1
+#define MK_NODE_MASTER 2
+
+typedef struct mk_net mk_net;
+
+typedef struct {
+    const char *name;    /* service name other nodes address it by          */
+    int kind;            /* MK_NODE_*                                        */
+    const char *program; /* TIS source for MK_NODE_PROGRAM (NULL = "")     */
+} mk_node_desc;
+
+#define MK_FLAG_STOP_ON_OUTPUT 1u
+
+typedef struct {
+    uint32_t budget;      /* retired node-instructions per lane; 0 = 1<<20          */
+    uint32_t stack_cap;   /* values per stack per lane; 0 = 1024                     */
+    uint32_t flags;       /* MK_FLAG_*                                               */
+    uint32_t device_mask; /* host API: GPUs to shard the batch over; 0 = GPU 0 only */
+} mk_opts;
+
+/* Parse + lower every program node and wire ports/stacks.
+ * Replaces: ProgramNode.LoadProgram (internal/nodes/program.go:178-193) ->
+ * tis.GenerateLabelMap / tis.Tokenize (internal/tis/tokenizer.go:11-106) for
+ * every node of NODE_INFO (cmd/app.go:31), plus the name resolution that the
+ * reference does per call with grpc.Dial (program.go:492,510,525).
+ * Parse errors return MK_EPARSE with "node <name>: <Go error text>" in err,
+ * where the Go text is byte-identical to the reference's
+ * ("Cannot repeat label", "line N, label 'L' was not declared",
+ *  "line N, '<instr>' not a valid instruction"). */
+int mk_net_load(const mk_node_desc *nodes, int n, mk_net **out, char *err, size_t err_len);
+
+void mk_net_free(mk_net *net);
+
+/* Evaluate n independent /compute inputs (host arrays).
+ * Replaces: the /compute handler (master.go:197-224) + GetInput/SendOutput
+ * (master.go:233-249) + the program/stack node loops (program.go:80-92,
+ * stack.go:95-155) for a batch.  in[i] is the strconv.Atoi value of the form
+ * field; it is truncated to int32 inside, as GetInput does (master.go:237).
+ * out[i] is the first OUT value (what /compute returns), status[i] the
+ * MK_ST_* byte, steps[i] (nullable) the retired node-instructions. */
+int mk_compute_batch(mk_net *net, const int64_t *in, size_t n, int32_t *out, uint8_t *status,
+                     uint32_t *steps, const mk_opts *opts);
+
+/* ---- device API (inputs/outputs already in HBM) ------------------------- */
+#define MK_IN_I64 0 /* data: const int64_t*                                   */
+#define MK_IN_I32 1 /* data: const int32_t*                                   */
+#define MK_IN_GEN 2 /* synthetic: x_i = gen(seed, offset + i), no input bytes */
+
+#define MK_GEN_FULL 0   /* (int32)splitmix64(seed^i); lanes i%16==15 take int32 edge values */
+#define MK_GEN_MASKED 1 /* splitmix64(seed^i) & mask                                          */
+
+typedef struct {
+    int kind;          /* MK_IN_*                               */
+    const void *data;  /* device pointer (MK_IN_I64 / MK_IN_I32) */
+    uint64_t seed;     /* MK_IN_GEN                             */
+    uint32_t gen_kind; /* MK_GEN_*                              */
+    uint32_t gen_mask;
+    uint64_t offset;   /* global lane index of element 0        */
+} mk_input;
+
+/* stats (nullable, device uint64[8], accumulated, caller zeroes):
+ * [0] retired node-instructions  [1] lanes with output  [2] lanes finished
+ * [3] quiescent  [4] budget  [5] stack overflow  [6] output-stop  [7] reserved */
+#define MK_STATS_LEN 8
+
+/* Launch the executor on `device` on HIP stream `stream` (NULL = default).
+ * d_out / d_status are required, d_steps / d_stats nullable.  Asynchronous. */
+int mk_compute_device(mk_net *net, int device, const mk_input *in, size_t n, int32_t *d_out,
+                      uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats,
+                      const mk_opts *opts, void *stream);
+
+/* Fill d_out[i] = gen(seed, offset + i) on device (same generator as MK_IN_GEN). */
+int mk_generate_inputs_device(int device, uint64_t seed, uint32_t gen_kind, uint32_t gen_mask,
+                              uint64_t offset, size_t n, int32_t *d_out, void *stream);
+
+/* ---- introspection -------------------------------------------------------- */
+/* Token dump of one program in the test format: lines joined by '\n', tokens
+ * by '\x1f' (the [][]string of tis.Tokenize); on error the Go error text and
+ * MK_EPARSE.  Replaces tis.Tokenize for parity tests. */
+int mk_tokenize(const char *program, char *out, size_t out_len);
+
+/* Lowered bytecode of a loaded network as text (one instruction per line). */
+int mk_net_disasm(const mk_net *net, char *out, size_t out_len);
+
+/* counts: [0] program nodes [1] stack nodes [2] total instructions */
+int mk_net_info(const mk_net *net, int *counts3);
+
+/* Integer-issue peak probe: launches a dependency-free v_add_u32 kernel doing
+ * `iters` x 64 adds per lane over blocks x 256 lanes; returns the lane-op count
+ * it performs in *lane_ops.  Caller times it with events on `stream`. */
+int mk_valu_probe_device(int device, int blocks, int iters, uint64_t *lane_ops, void *stream);
+
+const char *mk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MK_H */

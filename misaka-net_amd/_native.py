@@ -1,0 +1,145 @@
+"""ctypes binding of the C ABI declared in include/mk.h.
+
+The shared library is built in-tree (``misaka-net_amd/lib/libmisaka_amd.so``,
+see ``__graft_entry__.build``).  There is no fallback: if the library is
+missing every entry point raises, so a GPU run can never silently take a
+CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmisaka_amd.so")
+
+MK_OK = 0
+MK_EINVAL = -1
+MK_EPARSE = -2
+MK_ELIMIT = -3
+MK_EDEVICE = -4
+MK_ENOMEM = -5
+
+MK_ST_QUIESCENT = 1
+MK_ST_BUDGET = 2
+MK_ST_STACK_OVERFLOW = 3
+MK_ST_OUTPUT_STOP = 4
+MK_ST_REASON_MASK = 0x0F
+MK_ST_HAS_OUTPUT = 0x10
+
+MK_NODE_PROGRAM = 0
+MK_NODE_STACK = 1
+MK_NODE_MASTER = 2
+
+MK_FLAG_STOP_ON_OUTPUT = 1
+
+MK_IN_I64 = 0
+MK_IN_I32 = 1
+MK_IN_GEN = 2
+MK_GEN_FULL = 0
+MK_GEN_MASKED = 1
+MK_STATS_LEN = 8
+
+ERROR_NAMES = {
+    MK_EINVAL: "MK_EINVAL",
+    MK_EPARSE: "MK_EPARSE",
+    MK_ELIMIT: "MK_ELIMIT",
+    MK_EDEVICE: "MK_EDEVICE",
+    MK_ENOMEM: "MK_ENOMEM",
+}
+
+
+class mk_node_desc(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("kind", C.c_int), ("program", C.c_char_p)]
+
+
+class mk_opts(C.Structure):
+    _fields_ = [
+        ("budget", C.c_uint32),
+        ("stack_cap", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("device_mask", C.c_uint32),
+    ]
+
+
+class mk_input(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int),
+        ("data", C.c_void_p),
+        ("seed", C.c_uint64),
+        ("gen_kind", C.c_uint32),
+        ("gen_mask", C.c_uint32),
+        ("offset", C.c_uint64),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/mk.h declares.
+SIGNATURES = {
+    "mk_net_load": (C.c_int, [C.POINTER(mk_node_desc), C.c_int, C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t]),
+    "mk_net_free": (None, [C.c_void_p]),
+    "mk_compute_batch": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(mk_opts)],
+    ),
+    "mk_compute_device": (
+        C.c_int,
+        [
+            C.c_void_p,
+            C.c_int,
+            C.POINTER(mk_input),
+            C.c_size_t,
+            C.c_void_p,
+            C.c_void_p,
+            C.c_void_p,
+            C.c_void_p,
+            C.POINTER(mk_opts),
+            C.c_void_p,
+        ],
+    ),
+    "mk_generate_inputs_device": (
+        C.c_int,
+        [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p, C.c_void_p],
+    ),
+    "mk_tokenize": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "mk_net_disasm": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "mk_net_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    "mk_valu_probe_device": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
+    "mk_version": (C.c_char_p, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libmisaka_amd.so (raises NativeLibraryMissing if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryMissing(
+                    f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                )
+            h = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+        return _lib
+
+
+class MkError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}" if msg else ERROR_NAMES.get(code, str(code)))
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MK_OK:
+        raise MkError(rc, what)

@@ -1,0 +1,765 @@
+// mk_exec.hip -- CDNA4 (gfx950) batched executor for TIS networks + C ABI.
+//
+// One lane (work-item) evaluates one /compute input through a private copy
+// of the whole network (SURVEY.md section 8.0 lane model):
+//   * ACC/BAK (int64), the instruction pointer and the pending-send value of
+//     every program node live in VGPRs (the node loop is unrolled over the
+//     template bound NMAX, so every per-node array index is static);
+//   * port (R0..R3) values live in LDS rows [node*4+k][lane] -- any per-lane
+//     slot index is bank-conflict free because each lane owns one column --
+//     and their full bits in one 64-bit VGPR pair;
+//   * stacks keep their top W entries in an LDS ring per lane and spill older
+//     entries to HBM in a lane-major layout (coalesced when the lanes of a
+//     wave sit at the same depth);
+//   * the bytecode is read with wave-uniform (scalar) loads: for every node
+//     the wave "waterfalls" over the distinct instruction pointers present
+//     among its lanes, so the IP-uniform case (every lane at the same IP) is
+//     one iteration with a scalar decode, and divergent lanes (JEZ/JNZ/JGZ/
+//     JLZ/JRO on data) are handled group by group with ballots;
+//   * a lane that finishes (quiescent / budget / overflow / output-stop)
+//     writes its result and immediately takes the next input index
+//     (grid-stride refill), so data-dependent trip counts do not idle lanes.
+//
+// Semantics restated from internal/nodes/program.go:219-566,
+// internal/nodes/stack.go:95-155, internal/nodes/master.go:233-249 and
+// internal/utils/math.go:20-22; see tis_front.cpp for the lowering.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mk.h"
+#include "tis_front.h"
+
+namespace mk {
+
+constexpr int kBlock = 256;
+constexpr int kMaxDevices = 64;
+
+struct KParams {
+    uint32_t base[MK_MAX_PROGRAM_NODES];
+    uint32_t len[MK_MAX_PROGRAM_NODES];
+    int nprog;
+    int nstack;
+    int in_kind;
+    uint32_t gen_kind;
+    const void *in_data;
+    uint64_t seed;
+    uint64_t offset;
+    uint32_t gen_mask;
+    uint32_t budget;
+    uint64_t n;
+    int32_t *out;
+    uint8_t *status;
+    uint32_t *steps;
+    unsigned long long *stats;
+    uint32_t stack_cap;
+    uint32_t flags;
+    uint32_t ring;       // LDS ring entries per stack (power of two), 0 = no stacks
+    uint32_t spill_rows; // stack_cap - ring (HBM entries per stack per lane)
+    int32_t *spill;      // [nstack][spill_rows][lanes]
+    uint64_t lanes;      // resident lanes (grid threads)
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int32_t gen_value(uint64_t seed, uint32_t kind, uint32_t mask, uint64_t i)
+{
+    const uint64_t h = splitmix64(seed ^ i);
+    if (kind == MK_GEN_MASKED) return (int32_t)((uint32_t)h & mask);
+    if ((i & 15) == 15) {
+        switch ((h >> 32) & 7) {
+        case 0: return INT32_MIN;
+        case 1: return INT32_MIN + 1;
+        case 2: return INT32_MIN + 2;
+        case 3: return -1;
+        case 4: return 0;
+        case 5: return 1;
+        case 6: return INT32_MAX - 1;
+        default: return INT32_MAX;
+        }
+    }
+    return (int32_t)(uint32_t)h;
+}
+
+__device__ __forceinline__ int32_t lane_input(const KParams &p, uint64_t i)
+{
+    if (p.in_kind == MK_IN_I64) return (int32_t)((const int64_t *)p.in_data)[i]; // int32(v), master.go:237
+    if (p.in_kind == MK_IN_I32) return ((const int32_t *)p.in_data)[i];
+    return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Fetch one 16-byte instruction with a wave-uniform address as four dwords,
+// so it is a single scalar load (SMEM has no byte loads) and every decoded
+// field stays in SGPRs: the opcode switch is then a scalar branch.
+__device__ __forceinline__ Insn fetch(const Insn *__restrict__ code, uint32_t i)
+{
+    const uint4 w = reinterpret_cast<const uint4 *>(code)[i];
+    Insn I;
+    I.op = (uint8_t)(w.x & 0xffu);
+    I.src = (uint8_t)((w.x >> 8) & 0xffu);
+    I.dst = (uint8_t)((w.x >> 16) & 0xffu);
+    I.rsv0 = 0;
+    I.arg = (uint16_t)(w.y & 0xffffu);
+    I.rsv1 = 0;
+    I.imm = (int64_t)(((uint64_t)w.w << 32) | (uint64_t)w.z);
+    return I;
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code, KParams p)
+{
+    extern __shared__ int32_t lds[];
+    const int B = kBlock;
+    const int tid = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
+    int32_t *const port = lds;                       // [nprog*4][B]
+    int32_t *const sdepth = lds + p.nprog * 4 * B;   // [nstack][B]
+    int32_t *const ring = sdepth + p.nstack * B;     // [nstack][W][B]
+    const uint32_t W = p.ring;
+
+    int64_t acc[NMAX], bak[NMAX];
+    int32_t ip[NMAX], pendv[NMAX];
+    uint32_t pend = 0, hung = 0;
+    uint64_t pfull = 0;
+    bool in_avail = false;
+    int32_t in_val = 0, out_val = 0;
+    int out_cnt = 0;
+    uint32_t steps = 0;
+
+    unsigned long long s_steps = 0, s_out = 0, s_done = 0, s_q = 0, s_b = 0, s_ov = 0, s_os = 0;
+
+    uint64_t idx = gid;
+    bool active = idx < p.n;
+
+    auto init = [&](uint64_t i) {
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            acc[n] = 0; bak[n] = 0; ip[n] = 0; pendv[n] = 0;
+        }
+        pend = 0; hung = 0; pfull = 0;
+        in_avail = true;
+        in_val = lane_input(p, i);
+        out_cnt = 0; out_val = 0; steps = 0;
+        for (int s = 0; s < p.nstack; ++s) sdepth[s * B + tid] = 0;
+    };
+    if (active) init(idx);
+
+    while (__ballot(active) != 0ull) {
+        bool changed = false, done = false;
+        uint32_t reason = 0;
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            if (n >= p.nprog) continue; // wave-uniform; keeps the loop fully unrollable
+            const uint32_t len = p.len[n];
+            bool pending = active && !done && !((hung >> n) & 1u);
+            unsigned long long todo = __ballot(pending);
+            while (todo) {
+                const int lead = __builtin_ctzll(todo);
+                const int u = __builtin_amdgcn_readlane(ip[n], lead);
+                const bool mine = pending && ip[n] == u;
+                todo &= ~__ballot(mine);
+                const Insn I = fetch(code, p.base[n] + (uint32_t)u); // one s_load_dwordx4
+                if (!mine) continue;
+                pending = false;
+                auto retire = [&]() {
+                    ip[n] = (ip[n] + 1 == (int32_t)len) ? 0 : ip[n] + 1; // program.go:429
+                    ++steps;
+                    changed = true;
+                };
+                auto jump = [&](int32_t t) {
+                    ip[n] = t;
+                    ++steps;
+                    changed = true;
+                };
+                switch (I.op) {
+                case OP_NOP: retire(); break;
+                case OP_SWP: { const int64_t t = acc[n]; acc[n] = bak[n]; bak[n] = t; retire(); break; }
+                case OP_SAV: bak[n] = acc[n]; retire(); break;
+                case OP_NEG: acc[n] = (int64_t)(0ull - (uint64_t)acc[n]); retire(); break;
+                case OP_JMP: jump(I.arg); break;
+                case OP_JEZ: if (acc[n] == 0) jump(I.arg); else retire(); break;
+                case OP_JNZ: if (acc[n] != 0) jump(I.arg); else retire(); break;
+                case OP_JGZ: if (acc[n] > 0) jump(I.arg); else retire(); break;
+                case OP_JLZ: if (acc[n] < 0) jump(I.arg); else retire(); break;
+                case OP_STUCK: break;
+                case OP_IN:
+                    if (in_avail) { // <-m.inChan (master.go:235)
+                        in_avail = false;
+                        if (I.dst) acc[n] = in_val;
+                        retire();
+                    }
+                    break;
+                case OP_POP: {
+                    int32_t *dp = &sdepth[I.arg * B + tid];
+                    const int32_t d = *dp;
+                    if (d > 0) { // waitPop blocks while empty (stack.go:133-155)
+                        const uint32_t e = (uint32_t)d - 1;
+                        int32_t *rp = &ring[((uint32_t)I.arg * W + (e & (W - 1))) * B + tid];
+                        const int32_t v = *rp;
+                        if (e >= W)
+                            *rp = p.spill[((uint64_t)I.arg * p.spill_rows + (e - W)) * p.lanes + gid];
+                        *dp = (int32_t)e;
+                        if (I.dst) acc[n] = v;
+                        retire();
+                    }
+                    break;
+                }
+                default: {
+                    // Ops with a source operand: getFromSrc (program.go:434-472).
+                    const bool pn = (pend >> n) & 1u;
+                    int64_t v = 0;
+                    bool consumed = false;
+                    if (pn) {
+                        v = pendv[n];
+                    } else if (I.src == SRC_IMM) {
+                        v = I.imm;
+                    } else if (I.src == SRC_ACC) {
+                        v = acc[n];
+                    } else if (I.src >= SRC_R0) {
+                        const uint32_t slot = (uint32_t)n * 4 + (I.src - SRC_R0);
+                        if (!((pfull >> slot) & 1ull)) break; // receive blocks
+                        v = port[slot * B + tid];
+                        pfull &= ~(1ull << slot);
+                        consumed = true;
+                    }
+                    switch (I.op) {
+                    case OP_MOV: if (I.dst) acc[n] = v; retire(); break;
+                    case OP_ADD: acc[n] = (int64_t)((uint64_t)acc[n] + (uint64_t)v); retire(); break;
+                    case OP_SUB: acc[n] = (int64_t)((uint64_t)acc[n] - (uint64_t)v); retire(); break;
+                    case OP_JRO: {
+                        // IntClamp(ptr+v, 0, len-1), int64 wrapping add (program.go:354,362)
+                        int64_t t = (int64_t)((uint64_t)(int64_t)ip[n] + (uint64_t)v);
+                        t = t > (int64_t)len - 1 ? (int64_t)len - 1 : t;
+                        t = t < 0 ? 0 : t;
+                        jump((int32_t)t);
+                        break;
+                    }
+                    case OP_SEND: {
+                        const uint32_t slot = I.arg;
+                        if (!((pfull >> slot) & 1ull)) { // p.rK <- int32(v) (program.go:163,498)
+                            port[slot * B + tid] = (int32_t)v;
+                            pfull |= 1ull << slot;
+                            pend &= ~(1u << n);
+                            retire();
+                        } else if (!pn) {
+                            pend |= 1u << n;
+                            pendv[n] = (int32_t)v;
+                            changed = true;
+                        }
+                        break;
+                    }
+                    case OP_OUT:
+                        if (out_cnt < 2) { // outChan cap 1 + one /compute read (master.go:219,246)
+                            if (out_cnt == 0) out_val = (int32_t)v;
+                            ++out_cnt;
+                            pend &= ~(1u << n);
+                            retire();
+                            if (p.flags & MK_FLAG_STOP_ON_OUTPUT) { done = true; reason = MK_ST_OUTPUT_STOP; }
+                        } else if (!pn) {
+                            pend |= 1u << n;
+                            pendv[n] = (int32_t)v;
+                            changed = true;
+                        }
+                        break;
+                    case OP_PUSH: {
+                        int32_t *dp = &sdepth[I.arg * B + tid];
+                        const uint32_t d = (uint32_t)*dp;
+                        if (d >= p.stack_cap) { done = true; reason = MK_ST_STACK_OVERFLOW; break; }
+                        int32_t *rp = &ring[((uint32_t)I.arg * W + (d & (W - 1))) * B + tid];
+                        if (d >= W)
+                            p.spill[((uint64_t)I.arg * p.spill_rows + (d - W)) * p.lanes + gid] = *rp;
+                        *rp = (int32_t)v; // ValueMessage{int32(v)} (program.go:516)
+                        *dp = (int32_t)(d + 1);
+                        retire();
+                        break;
+                    }
+                    case OP_HANG: hung |= 1u << n; changed = true; break;
+                    case OP_RETRY: if (consumed) changed = true; break;
+                    default: break;
+                    }
+                    break;
+                }
+                }
+            }
+        }
+        if (active && !done) {
+            if (!changed) { done = true; reason = MK_ST_QUIESCENT; }
+            else if (steps >= p.budget) { done = true; reason = MK_ST_BUDGET; }
+        }
+        if (done) {
+            const uint32_t st = reason | (out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0u);
+            p.out[idx] = out_cnt > 0 ? out_val : 0;
+            p.status[idx] = (uint8_t)st;
+            if (p.steps) p.steps[idx] = steps;
+            s_steps += steps;
+            s_out += out_cnt > 0;
+            s_done += 1;
+            s_q += reason == MK_ST_QUIESCENT;
+            s_b += reason == MK_ST_BUDGET;
+            s_ov += reason == MK_ST_STACK_OVERFLOW;
+            s_os += reason == MK_ST_OUTPUT_STOP;
+            idx += p.lanes;
+            active = idx < p.n;
+            if (active) init(idx);
+        }
+    }
+
+    if (p.stats) {
+        const unsigned long long v0 = wave_sum(s_steps), v1 = wave_sum(s_out), v2 = wave_sum(s_done),
+                                 v3 = wave_sum(s_q), v4 = wave_sum(s_b), v5 = wave_sum(s_ov),
+                                 v6 = wave_sum(s_os);
+        if ((tid & 63) == 0 && v2) {
+            atomicAdd(&p.stats[0], v0);
+            atomicAdd(&p.stats[1], v1);
+            atomicAdd(&p.stats[2], v2);
+            if (v3) atomicAdd(&p.stats[3], v3);
+            if (v4) atomicAdd(&p.stats[4], v4);
+            if (v5) atomicAdd(&p.stats[5], v5);
+            if (v6) atomicAdd(&p.stats[6], v6);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
+                                                     uint64_t offset, uint64_t n, int32_t *out)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = gen_value(seed, kind, mask, offset + i);
+}
+
+// Dependency-free integer adds: 8 independent chains x 8 adds per iteration.
+__global__ void __launch_bounds__(kBlock) valu_probe(int iters, uint32_t *sink)
+{
+    uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
+             a6 = a0 + 6, a7 = a0 + 7;
+    const uint32_t c = blockIdx.x | 1u;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            asm volatile("v_add_u32 %0, %0, %8\n\t"
+                         "v_add_u32 %1, %1, %8\n\t"
+                         "v_add_u32 %2, %2, %8\n\t"
+                         "v_add_u32 %3, %3, %8\n\t"
+                         "v_add_u32 %4, %4, %8\n\t"
+                         "v_add_u32 %5, %5, %8\n\t"
+                         "v_add_u32 %6, %6, %8\n\t"
+                         "v_add_u32 %7, %7, %8"
+                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                         : "v"(c));
+        }
+    }
+    if ((a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) == 0x9E3779B9u) sink[0] = 1;
+}
+
+// ------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------
+struct DevCtx {
+    bool ready = false;
+    Insn *d_code = nullptr;
+    int cus = 0;
+    int32_t *d_spill = nullptr;
+    size_t spill_bytes = 0;
+    void *d_stage = nullptr; // host-API staging buffer
+    size_t stage_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+} // namespace mk
+
+struct mk_net {
+    mk::Network net;
+    std::mutex mu;      // serialises host-API calls and device-context setup
+    mk::DevCtx dev[mk::kMaxDevices];
+    ~mk_net()
+    {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        for (int d = 0; d < mk::kMaxDevices; d++) {
+            mk::DevCtx &c = dev[d];
+            if (!c.ready) continue;
+            (void)hipSetDevice(d);
+            if (c.stream) (void)hipStreamSynchronize(c.stream);
+            (void)hipFree(c.d_code);
+            (void)hipFree(c.d_spill);
+            (void)hipFree(c.d_stage);
+            if (c.stream) (void)hipStreamDestroy(c.stream);
+        }
+        (void)hipSetDevice(prev);
+    }
+};
+
+namespace mk {
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int device_count()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// Caller holds net->mu.
+int ensure_device(mk_net *h, int d)
+{
+    DevCtx &c = h->dev[d];
+    if (c.ready) return MK_OK;
+    DeviceGuard g(d);
+    const size_t bytes = h->net.code.size() * sizeof(Insn);
+    if (hipMalloc(&c.d_code, bytes) != hipSuccess) return MK_ENOMEM;
+    if (hipMemcpy(c.d_code, h->net.code.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return MK_EDEVICE;
+    if (hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) return MK_EDEVICE;
+    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) return MK_EDEVICE;
+    c.ready = true;
+    return MK_OK;
+}
+
+template <int NMAX>
+void *kernel_ptr() { return reinterpret_cast<void *>(&tis_exec<NMAX>); }
+
+void *pick_kernel(int nprog)
+{
+    if (nprog <= 1) return kernel_ptr<1>();
+    if (nprog <= 2) return kernel_ptr<2>();
+    if (nprog <= 4) return kernel_ptr<4>();
+    if (nprog <= 8) return kernel_ptr<8>();
+    return kernel_ptr<16>();
+}
+
+struct Launch {
+    void *fn;
+    int blocks;
+    size_t lds;
+    uint32_t ring;
+};
+
+// Shape the launch: LDS ring depth, dynamic LDS bytes, resident grid.
+int plan_launch(const Network &net, const DevCtx &c, size_t n, uint32_t stack_cap, Launch &L)
+{
+    L.fn = pick_kernel(net.nprog);
+    uint32_t ring = 0;
+    int stack_rows = 0;
+    if (net.uses_stacks) {
+        // Keep >= 2 blocks per CU: <= 80 KiB of LDS per 256-lane block.
+        ring = 16;
+        while (ring > 1 && (size_t)(net.nprog * 4 + net.nstack * (1 + ring)) * kBlock * 4 > 80 * 1024) ring >>= 1;
+        stack_rows = net.nstack;
+    }
+    const size_t lds = (size_t)(net.nprog * 4 + stack_rows * (1 + ring)) * kBlock * 4;
+    if (lds > 160 * 1024) return MK_ELIMIT;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, L.fn, kBlock, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint64_t want = (n + kBlock - 1) / kBlock;
+    const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(c.cus, 1);
+    L.blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    L.lds = lds;
+    L.ring = ring;
+    (void)stack_cap;
+    return MK_OK;
+}
+
+void resolve_opts(const mk_opts *o, uint32_t &budget, uint32_t &cap, uint32_t &flags)
+{
+    budget = (o && o->budget) ? o->budget : (1u << 20);
+    if (budget > 0xFFFFFF00u) budget = 0xFFFFFF00u; // steps (u32) may overshoot by < 16
+    cap = (o && o->stack_cap) ? o->stack_cap : 1024u;
+    flags = o ? o->flags : 0u;
+}
+
+// Caller holds h->mu.  Asynchronous on `stream`.
+int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,
+                  uint32_t *d_steps, uint64_t *d_stats, const mk_opts *o, hipStream_t stream)
+{
+    if (n == 0) return MK_OK;
+    int rc = ensure_device(h, d);
+    if (rc) return rc;
+    DevCtx &c = h->dev[d];
+    DeviceGuard g(d);
+    uint32_t budget, cap, flags;
+    resolve_opts(o, budget, cap, flags);
+    Launch L;
+    if ((rc = plan_launch(h->net, c, n, cap, L))) return rc;
+    const uint64_t lanes = (uint64_t)L.blocks * kBlock;
+    uint32_t spill_rows = 0;
+    if (h->net.uses_stacks && cap > L.ring) {
+        spill_rows = cap - L.ring;
+        const size_t need = (size_t)h->net.nstack * spill_rows * lanes * sizeof(int32_t);
+        if (need > c.spill_bytes) {
+            if (c.d_spill) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(c.d_spill);
+                c.d_spill = nullptr;
+                c.spill_bytes = 0;
+            }
+            if (hipMalloc(&c.d_spill, need) != hipSuccess) return MK_ENOMEM;
+            c.spill_bytes = need;
+        }
+    }
+    KParams p{};
+    for (int i = 0; i < h->net.nprog; i++) {
+        p.base[i] = h->net.base[i];
+        p.len[i] = h->net.len[i];
+    }
+    p.nprog = h->net.nprog;
+    p.nstack = h->net.uses_stacks ? h->net.nstack : 0;
+    p.in_kind = in->kind;
+    p.in_data = in->data;
+    p.seed = in->seed;
+    p.gen_kind = in->gen_kind;
+    p.gen_mask = in->gen_mask;
+    p.offset = in->offset;
+    p.n = n;
+    p.out = d_out;
+    p.status = d_status;
+    p.steps = d_steps;
+    p.stats = reinterpret_cast<unsigned long long *>(d_stats);
+    p.budget = budget;
+    p.stack_cap = cap;
+    p.flags = flags;
+    p.ring = L.ring;
+    p.spill_rows = spill_rows;
+    p.spill = c.d_spill;
+    p.lanes = lanes;
+    const Insn *code = c.d_code;
+    void *args[] = {(void *)&code, (void *)&p};
+    if (hipLaunchKernel(L.fn, dim3(L.blocks), dim3(kBlock), args, L.lds, stream) != hipSuccess)
+        return MK_EDEVICE;
+    return MK_OK;
+}
+
+void set_err(char *err, size_t len, const std::string &s)
+{
+    if (!err || !len) return;
+    size_t k = std::min(len - 1, s.size());
+    memcpy(err, s.data(), k);
+    err[k] = 0;
+}
+
+int copy_out(char *out, size_t len, const std::string &s)
+{
+    if (!out || !len) return MK_EINVAL;
+    set_err(out, len, s);
+    return s.size() < len ? MK_OK : MK_EINVAL;
+}
+
+} // namespace
+} // namespace mk
+
+// ------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------
+extern "C" {
+
+const char *mk_version(void) { return "misaka-net-amd 0.1.0 (gfx950)"; }
+
+int mk_net_load(const mk_node_desc *nodes, int n, mk_net **out, char *err, size_t err_len)
+{
+    if (!nodes || n <= 0 || !out) {
+        mk::set_err(err, err_len, "invalid arguments");
+        return MK_EINVAL;
+    }
+    *out = nullptr;
+    std::vector<mk::NodeSpec> specs;
+    for (int i = 0; i < n; i++) {
+        if (!nodes[i].name) {
+            mk::set_err(err, err_len, "node without a name");
+            return MK_EINVAL;
+        }
+        specs.push_back({nodes[i].name, nodes[i].kind, nodes[i].program ? nodes[i].program : ""});
+    }
+    mk_net *h = new (std::nothrow) mk_net();
+    if (!h) return MK_ENOMEM;
+    std::string e;
+    int rc = mk::lower_network(specs, h->net, e);
+    if (rc) {
+        mk::set_err(err, err_len, e);
+        delete h;
+        return rc;
+    }
+    mk::set_err(err, err_len, "");
+    *out = h;
+    return MK_OK;
+}
+
+void mk_net_free(mk_net *net) { delete net; }
+
+int mk_compute_batch(mk_net *h, const int64_t *in, size_t n, int32_t *out, uint8_t *status, uint32_t *steps,
+                     const mk_opts *opts)
+{
+    if (!h || (n && (!in || !out || !status))) return MK_EINVAL;
+    if (n == 0) return MK_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    std::vector<int> devs;
+    const uint32_t mask = opts ? opts->device_mask : 0u;
+    if (mask == 0) devs.push_back(0);
+    for (int d = 0; d < ndev && d < 32; d++)
+        if (mask & (1u << d)) devs.push_back(d);
+    if (devs.empty()) return MK_EINVAL;
+    const size_t G = devs.size();
+    struct Shard { int d; size_t lo, hi; int64_t *din; int32_t *dout; uint8_t *dst; uint32_t *dsteps; };
+    std::vector<Shard> sh;
+    for (size_t g = 0; g < G; g++) {
+        Shard s{devs[g], n * g / G, n * (g + 1) / G, nullptr, nullptr, nullptr, nullptr};
+        if (s.hi > s.lo) sh.push_back(s);
+    }
+    for (auto &s : sh) {
+        int rc = mk::ensure_device(h, s.d);
+        if (rc) return rc;
+        mk::DevCtx &c = h->dev[s.d];
+        mk::DeviceGuard g(s.d);
+        const size_t m = s.hi - s.lo;
+        const size_t a8 = (m * 8 + 255) & ~(size_t)255, a4 = (m * 4 + 255) & ~(size_t)255,
+                     a1 = (m + 255) & ~(size_t)255;
+        const size_t need = a8 + a4 + a4 + a1;
+        if (need > c.stage_bytes) {
+            (void)hipStreamSynchronize(c.stream);
+            (void)hipFree(c.d_stage);
+            c.d_stage = nullptr;
+            c.stage_bytes = 0;
+            if (hipMalloc(&c.d_stage, need) != hipSuccess) return MK_ENOMEM;
+            c.stage_bytes = need;
+        }
+        char *base = (char *)c.d_stage;
+        s.din = (int64_t *)base;
+        s.dout = (int32_t *)(base + a8);
+        s.dsteps = (uint32_t *)(base + a8 + a4);
+        s.dst = (uint8_t *)(base + a8 + a4 + a4);
+        if (hipMemcpyAsync(s.din, in + s.lo, m * 8, hipMemcpyHostToDevice, c.stream) != hipSuccess)
+            return MK_EDEVICE;
+        mk_input mi{};
+        mi.kind = MK_IN_I64;
+        mi.data = s.din;
+        rc = mk::launch_locked(h, s.d, &mi, m, s.dout, s.dst, steps ? s.dsteps : nullptr, nullptr, opts, c.stream);
+        if (rc) return rc;
+        if (hipMemcpyAsync(out + s.lo, s.dout, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+            hipMemcpyAsync(status + s.lo, s.dst, m, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
+            return MK_EDEVICE;
+        if (steps && hipMemcpyAsync(steps + s.lo, s.dsteps, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
+            return MK_EDEVICE;
+    }
+    int rc = MK_OK;
+    for (auto &s : sh) {
+        mk::DeviceGuard g(s.d);
+        if (hipStreamSynchronize(h->dev[s.d].stream) != hipSuccess) rc = MK_EDEVICE;
+    }
+    return rc;
+}
+
+int mk_compute_device(mk_net *h, int device, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,
+                      uint32_t *d_steps, uint64_t *d_stats, const mk_opts *opts, void *stream)
+{
+    if (!h || !in || (n && (!d_out || !d_status))) return MK_EINVAL;
+    if (in->kind != MK_IN_GEN && n && !in->data) return MK_EINVAL;
+    if (in->kind < MK_IN_I64 || in->kind > MK_IN_GEN) return MK_EINVAL;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev || device >= mk::kMaxDevices) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return mk::launch_locked(h, device, in, n, d_out, d_status, d_steps, d_stats, opts, (hipStream_t)stream);
+}
+
+int mk_generate_inputs_device(int device, uint64_t seed, uint32_t gen_kind, uint32_t gen_mask, uint64_t offset,
+                              size_t n, int32_t *d_out, void *stream)
+{
+    if (n == 0) return MK_OK;
+    if (!d_out) return MK_EINVAL;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev) return MK_EINVAL;
+    mk::DeviceGuard g(device);
+    const uint64_t blocks = std::min<uint64_t>((n + mk::kBlock - 1) / mk::kBlock, 8192);
+    hipLaunchKernelGGL(mk::gen_inputs, dim3((unsigned)blocks), dim3(mk::kBlock), 0, (hipStream_t)stream, seed,
+                       gen_kind, gen_mask, offset, (uint64_t)n, d_out);
+    return hipGetLastError() == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+
+int mk_valu_probe_device(int device, int blocks, int iters, uint64_t *lane_ops, void *stream)
+{
+    if (blocks <= 0 || iters <= 0) return MK_EINVAL;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev) return MK_EINVAL;
+    mk::DeviceGuard g(device);
+    static uint32_t *sink[mk::kMaxDevices] = {};
+    static std::mutex smu;
+    {
+        std::lock_guard<std::mutex> lk(smu);
+        if (!sink[device] && hipMalloc(&sink[device], 4) != hipSuccess) return MK_ENOMEM;
+    }
+    hipLaunchKernelGGL(mk::valu_probe, dim3(blocks), dim3(mk::kBlock), 0, (hipStream_t)stream, iters, sink[device]);
+    if (lane_ops) *lane_ops = (uint64_t)blocks * mk::kBlock * (uint64_t)iters * 64u;
+    return hipGetLastError() == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+
+int mk_tokenize(const char *program, char *out, size_t out_len)
+{
+    if (!program || !out || !out_len) return MK_EINVAL;
+    mk::Program P;
+    std::string err;
+    if (!mk::parse_program(program, P, err)) {
+        mk::set_err(out, out_len, err);
+        return MK_EPARSE;
+    }
+    std::string s;
+    for (size_t i = 0; i < P.lines.size(); i++) {
+        if (i) s += '\n';
+        s += mk::form_name(P.lines[i].form);
+        if (!P.lines[i].a.empty()) { s += '\x1f'; s += P.lines[i].a; }
+        if (!P.lines[i].b.empty()) { s += '\x1f'; s += P.lines[i].b; }
+    }
+    return mk::copy_out(out, out_len, s);
+}
+
+int mk_net_disasm(const mk_net *net, char *out, size_t out_len)
+{
+    if (!net) return MK_EINVAL;
+    return mk::copy_out(out, out_len, mk::disasm(net->net));
+}
+
+int mk_net_info(const mk_net *net, int *counts3)
+{
+    if (!net || !counts3) return MK_EINVAL;
+    counts3[0] = net->net.nprog;
+    counts3[1] = net->net.nstack;
+    counts3[2] = (int)net->net.code.size();
+    return MK_OK;
+}
+
+} // extern "C"

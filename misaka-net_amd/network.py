@@ -1,0 +1,188 @@
+"""Host-side mirror of the reference's node network for the batched /compute path.
+
+``Network`` replaces the set of ``ProgramNode``/``StackNode`` processes of a
+deployment (internal/nodes/program.go, internal/nodes/stack.go; topology from
+NODE_INFO, cmd/app.go:31, and each node's PROGRAM, cmd/app.go:21) by one
+loaded ``mk_net`` handle.  ``compute_batch`` evaluates many independent
+``/compute`` inputs (master.go:197-224) at once on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Iterable, Mapping, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+STATUS_NAMES = {
+    N.MK_ST_QUIESCENT: "quiescent",
+    N.MK_ST_BUDGET: "budget",
+    N.MK_ST_STACK_OVERFLOW: "stack_overflow",
+    N.MK_ST_OUTPUT_STOP: "output_stop",
+}
+
+
+class TisParseError(ValueError):
+    """A program was rejected; ``str(e)`` is the reference's Go error text."""
+
+
+def tokenize(program: str) -> list[list[str]]:
+    """tis.Tokenize (internal/tis/tokenizer.go:29-106) on one program: the
+    ``[][]string`` the reference builds, or TisParseError with its message."""
+    buf = C.create_string_buffer(max(4096, 64 * len(program) + 1024))
+    rc = N.lib().mk_tokenize(program.encode(), buf, len(buf))
+    text = buf.value.decode(errors="surrogateescape")
+    if rc == N.MK_EPARSE:
+        raise TisParseError(text)
+    N.check(rc, "mk_tokenize")
+    return [line.split("\x1f") for line in text.split("\n")]
+
+
+@dataclass
+class NodeSpec:
+    name: str
+    kind: str = "program"  # "program" | "stack" | "master"
+    program: str = ""
+
+
+_KINDS = {"program": N.MK_NODE_PROGRAM, "stack": N.MK_NODE_STACK, "master": N.MK_NODE_MASTER}
+
+
+@dataclass
+class BatchResult:
+    out: np.ndarray  # int32: first OUT value (the /compute result), 0 if none
+    status: np.ndarray  # uint8: MK_ST_* reason | MK_ST_HAS_OUTPUT
+    steps: Optional[np.ndarray]  # uint32 retired node-instructions, if requested
+
+    @property
+    def has_output(self) -> np.ndarray:
+        return (self.status & N.MK_ST_HAS_OUTPUT) != 0
+
+    @property
+    def reason(self) -> np.ndarray:
+        return self.status & N.MK_ST_REASON_MASK
+
+
+def make_opts(budget=None, stack_cap=None, stop_on_output=False, devices: Optional[Iterable[int]] = None):
+    o = N.mk_opts()
+    o.budget = int(budget or 0)
+    o.stack_cap = int(stack_cap or 0)
+    o.flags = N.MK_FLAG_STOP_ON_OUTPUT if stop_on_output else 0
+    mask = 0
+    for d in devices or ():
+        mask |= 1 << int(d)
+    o.device_mask = mask
+    return o
+
+
+class Network:
+    """A loaded network.
+
+    ``nodes`` is a sequence of NodeSpec (or ``(name, kind, program)`` tuples).
+    Program nodes are executed in sorted-name order (the canonical schedule).
+    """
+
+    def __init__(self, nodes: Sequence):
+        specs = [n if isinstance(n, NodeSpec) else NodeSpec(*n) for n in nodes]
+        arr = (N.mk_node_desc * len(specs))()
+        self._keep = []
+        for i, s in enumerate(specs):
+            if s.kind not in _KINDS:
+                raise ValueError(f"invalid node type {s.kind!r}")
+            nm, pg = s.name.encode(), (s.program or "").encode()
+            self._keep += [nm, pg]
+            arr[i].name, arr[i].kind, arr[i].program = nm, _KINDS[s.kind], pg
+        h = C.c_void_p()
+        err = C.create_string_buffer(8192)
+        rc = N.lib().mk_net_load(arr, len(specs), C.byref(h), err, len(err))
+        if rc == N.MK_EPARSE:
+            raise TisParseError(err.value.decode(errors="surrogateescape"))
+        N.check(rc, err.value.decode(errors="surrogateescape"))
+        self._h = h
+        self.specs = specs
+
+    @classmethod
+    def from_node_info(cls, node_info: Mapping[str, Mapping], programs: Mapping[str, str], master: Optional[str] = None):
+        """Build from the master's NODE_INFO JSON (docker-compose.yml:16-21) and
+        each program node's PROGRAM env var (cmd/app.go:21)."""
+        nodes = [NodeSpec(name, info["type"], programs.get(name, "")) for name, info in node_info.items()]
+        if master:
+            nodes.append(NodeSpec(master, "master"))
+        return cls(nodes)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().mk_net_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def info(self):
+        c = (C.c_int * 3)()
+        N.check(N.lib().mk_net_info(self._h, c))
+        return {"program_nodes": c[0], "stack_nodes": c[1], "instructions": c[2]}
+
+    def disasm(self) -> str:
+        buf = C.create_string_buffer(1 << 20)
+        N.check(N.lib().mk_net_disasm(self._h, buf, len(buf)))
+        return buf.value.decode()
+
+    def compute_batch(self, values, *, budget=None, stack_cap=None, stop_on_output=False, devices=None, steps=True):
+        """Evaluate independent /compute inputs (strconv.Atoi int64 values,
+        truncated to int32 at GetInput like master.go:237) on the GPU(s)."""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        n = v.size
+        out = np.zeros(n, np.int32)
+        st = np.zeros(n, np.uint8)
+        sp = np.zeros(n, np.uint32) if steps else None
+        o = make_opts(budget, stack_cap, stop_on_output, devices)
+        rc = N.lib().mk_compute_batch(
+            self._h,
+            v.ctypes.data_as(C.c_void_p),
+            n,
+            out.ctypes.data_as(C.c_void_p),
+            st.ctypes.data_as(C.c_void_p),
+            sp.ctypes.data_as(C.c_void_p) if sp is not None else None,
+            C.byref(o),
+        )
+        N.check(rc, "mk_compute_batch")
+        return BatchResult(out, st, sp)
+
+    def compute_device(self, n, *, out_ptr, status_ptr, steps_ptr=None, stats_ptr=None, device=0, stream=None,
+                       in_ptr=None, in_kind=N.MK_IN_I32, seed=0, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0,
+                       budget=None, stack_cap=None, stop_on_output=False):
+        """Launch on device memory (raw pointers, e.g. torch ``data_ptr()``);
+        asynchronous on ``stream`` (a HIP stream handle, e.g.
+        ``torch.cuda.current_stream().cuda_stream``)."""
+        mi = N.mk_input()
+        mi.kind = N.MK_IN_GEN if in_ptr is None else in_kind
+        mi.data = in_ptr
+        mi.seed = seed
+        mi.gen_kind = gen_kind
+        mi.gen_mask = gen_mask
+        mi.offset = offset
+        o = make_opts(budget, stack_cap, stop_on_output)
+        rc = N.lib().mk_compute_device(
+            self._h, device, C.byref(mi), n, out_ptr, status_ptr, steps_ptr, stats_ptr, C.byref(o), stream
+        )
+        N.check(rc, "mk_compute_device")
+
+
+def generate_inputs_device(n, out_ptr, *, seed, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0, device=0, stream=None):
+    N.check(N.lib().mk_generate_inputs_device(device, seed, gen_kind, gen_mask, offset, n, out_ptr, stream))
+
+
+def valu_probe_device(blocks, iters, *, device=0, stream=None) -> int:
+    ops = C.c_uint64()
+    N.check(N.lib().mk_valu_probe_device(device, blocks, iters, C.byref(ops), stream))
+    return ops.value

@@ -1,0 +1,138 @@
+"""The networks of BASELINE.json's five configs.
+
+C1/C2  docker-compose example network (docker-compose.yml:35-40,54-59): the
+       YAML ``|`` block keeps one trailing newline, so each program has a
+       sixth, empty line that executes as NOP.  README.md:39-44: result x+2.
+C3     network built around docs/sample.txt "Example 2" (sample.txt:20-29),
+       which is not loadable verbatim: ``entry`` feeds the
+       input to ``router`` (sample.txt:20-29 verbatim, comp1:R1 -> pos:R3 and
+       comp1:R3 -> neg:R3); ``pos``/``neg`` run sample.txt:2-3 without the
+       ``//`` comments (MOV R3, ACC / ADD ACC) then OUT ACC.  Zero input ->
+       no output (quiescent); otherwise int32(2x).
+C4     8-program-node pipeline; node k pushes D values to its own stack,
+       pops them back folding sum = 4*sum + v (ports used as scratch), and forwards the
+       int32 sum to node k+1; the last node outputs.
+C5     data-dependent countdown (``L: SUB 1 / JGZ L``) feeding a JRO-dispatched
+       digit loop: trip counts follow the input, lanes diverge.
+"""
+from __future__ import annotations
+
+from .network import NodeSpec
+
+EXAMPLE_MISAKA1 = "IN ACC\nADD 1\nMOV ACC, misaka2:R0\nMOV R0, ACC\nOUT ACC\n"
+EXAMPLE_MISAKA2 = "MOV R0, ACC\nADD 1\nPUSH ACC, misaka3\nPOP misaka3, ACC\nMOV ACC, misaka1:R0\n"
+
+
+def example_network():
+    """docker-compose.yml: master last_order, programs misaka1/misaka2, stack misaka3."""
+    return [
+        NodeSpec("misaka1", "program", EXAMPLE_MISAKA1),
+        NodeSpec("misaka2", "program", EXAMPLE_MISAKA2),
+        NodeSpec("misaka3", "stack"),
+        NodeSpec("last_order", "master"),
+    ]
+
+
+SAMPLE_ROUTER = (
+    "START:\n"
+    "    MOV R0, ACC\n"
+    "    JGZ POSITIVE\n"
+    "    JLZ NEGATIVE\n"
+    "    JMP START\n"
+    "POSITIVE: MOV ACC, pos:R3\n"
+    "    JMP START\n"
+    "NEGATIVE:\n"
+    "    MOV ACC, neg:R3\n"
+    "    JMP START\n"
+)
+SAMPLE_DOUBLER = "MOV R3, ACC\nADD ACC\nOUT ACC\n"
+
+
+def sample_network():
+    return [
+        NodeSpec("entry", "program", "IN ACC\nMOV ACC, router:R0\n"),
+        NodeSpec("router", "program", SAMPLE_ROUTER),
+        NodeSpec("pos", "program", SAMPLE_DOUBLER),
+        NodeSpec("neg", "program", SAMPLE_DOUBLER),
+        NodeSpec("master", "master"),
+    ]
+
+
+def pipeline_program(k: int, nodes: int, depth: int) -> str:
+    me, stk = f"p{k}", f"s{k}"
+    first = "IN ACC" if k == 0 else "MOV R0, ACC"
+    last = "OUT ACC" if k == nodes - 1 else f"MOV ACC, p{k + 1}:R0"
+    return "\n".join(
+        [
+            first,
+            "SAV",  # BAK = x
+            f"MOV {depth}, ACC",
+            "PL: SWP",  # ACC = x+i, BAK = counter
+            "ADD 1",
+            f"PUSH ACC, {stk}",
+            "SWP",
+            "SUB 1",
+            "JGZ PL",
+            "MOV 0, ACC",
+            "SAV",  # BAK = running sum
+            f"MOV {depth}, ACC",
+            f"MOV ACC, {me}:R1",  # counter kept in own port R1
+            f"QL: POP {stk}, ACC",
+            f"MOV ACC, {me}:R2",
+            "SWP",
+            "ADD ACC",  # sum = 4*sum + v: order dependent, so LIFO order is checked
+            "ADD ACC",
+            "ADD R2",
+            "SAV",
+            "MOV R1, ACC",
+            "SUB 1",
+            f"MOV ACC, {me}:R1",
+            "JGZ QL",
+            "MOV R1, NIL",  # drain the counter port
+            "SWP",
+            last,
+            "",
+        ]
+    )
+
+
+def pipeline_network(depth: int = 64, nodes: int = 8):
+    out = [NodeSpec(f"p{k}", "program", pipeline_program(k, nodes, depth)) for k in range(nodes)]
+    out += [NodeSpec(f"s{k}", "stack") for k in range(nodes)]
+    return out
+
+
+COUNTDOWN = "IN ACC\nSAV\nL: SUB 1\nJGZ L\nSWP\nMOV ACC, digits:R0\n"
+# Repeatedly subtract 3; the remainder (1..3) selects one of three ADDs via JRO.
+DIGITS = (
+    "MOV R0, ACC\n"
+    "JEZ Z\n"
+    "JLZ Z\n"
+    "L: SUB 3\n"
+    "JGZ L\n"
+    "ADD 3\n"
+    "JRO ACC\n"
+    "ADD 100\n"
+    "ADD 10\n"
+    "ADD 1\n"
+    "OUT ACC\n"
+    "JMP E\n"
+    "Z: OUT -1\n"
+    "E: NOP\n"
+)
+
+
+def countdown_network():
+    return [
+        NodeSpec("count", "program", COUNTDOWN),
+        NodeSpec("digits", "program", DIGITS),
+    ]
+
+
+CONFIGS = {
+    "c1_example_cpu": example_network,
+    "c2_example": example_network,
+    "c3_sample": sample_network,
+    "c4_pipeline": pipeline_network,
+    "c5_countdown": countdown_network,
+}

@@ -1,0 +1,157 @@
+"""ctypes binding of the C oracle (oracle/tis_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- the parity checker.  Imported by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the product
+package (misaka-net_amd/).  See tis_oracle.c's header for what pins it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "tis_oracle.c")
+LIB = os.path.join(HERE, "build", "liboracle_tis.so")
+
+ST_QUIESCENT, ST_BUDGET, ST_STACK_OVERFLOW, ST_OUTPUT_STOP, ST_HAS_OUTPUT = 1, 2, 3, 4, 0x10
+KIND = {"program": 0, "stack": 1}
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with gcc (no GPU needed)."""
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        subprocess.check_call(
+            ["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-pthread", "-o", LIB, SRC]
+        )
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        h = C.CDLL(LIB)
+        h.orc_tokenize.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+        h.orc_label_map.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+        h.orc_net_load.restype = C.c_void_p
+        h.orc_net_load.argtypes = [
+            C.c_int,
+            C.POINTER(C.c_char_p),
+            C.POINTER(C.c_int),
+            C.POINTER(C.c_char_p),
+            C.c_char_p,
+            C.c_char_p,
+            C.c_size_t,
+        ]
+        h.orc_net_free.argtypes = [C.c_void_p]
+        h.orc_compute_batch.argtypes = [
+            C.c_void_p,
+            C.c_void_p,
+            C.c_size_t,
+            C.c_void_p,
+            C.c_void_p,
+            C.c_void_p,
+            C.c_uint32,
+            C.c_uint32,
+            C.c_int,
+            C.c_int,
+        ]
+        h.orc_gen_inputs.argtypes = [C.c_uint64, C.c_int, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p]
+        h.orc_go_atoi.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64)]
+        _lib = h
+    return _lib
+
+
+class OracleParseError(ValueError):
+    pass
+
+
+def tokenize(program: str) -> list[list[str]]:
+    buf = C.create_string_buffer(max(4096, 64 * len(program) + 1024))
+    rc = lib().orc_tokenize(program.encode(), buf, len(buf))
+    text = buf.value.decode(errors="surrogateescape")
+    if rc == -1:
+        raise OracleParseError(text)
+    assert rc == 0, "token buffer too small"
+    return [line.split("\x1f") for line in text.split("\n")]
+
+
+def label_map(program: str) -> dict:
+    buf = C.create_string_buffer(1 << 16)
+    rc = lib().orc_label_map(program.encode(), buf, len(buf))
+    if rc == -1:
+        raise OracleParseError(buf.value.decode())
+    out = {}
+    for line in buf.value.decode().splitlines():
+        k, v = line.rsplit("=", 1)
+        out[k] = int(v)
+    return out
+
+
+def go_atoi(s: str):
+    """strconv.Atoi restatement: returns int or raises ValueError."""
+    v = C.c_int64()
+    b = s.encode()
+    rc = lib().orc_go_atoi(b, len(b), C.byref(v))
+    if rc:
+        raise ValueError(f"strconv.Atoi: parsing {s!r}: {'invalid syntax' if rc == 1 else 'value out of range'}")
+    return v.value
+
+
+class OracleNet:
+    """nodes: sequence of objects with .name/.kind/.program (or tuples)."""
+
+    def __init__(self, nodes: Sequence):
+        rows = [(n.name, n.kind, n.program) if hasattr(n, "name") else tuple(n) for n in nodes]
+        master = [r[0] for r in rows if r[1] == "master"]
+        rows = [r for r in rows if r[1] != "master"]
+        n = len(rows)
+        names = (C.c_char_p * n)(*[r[0].encode() for r in rows])
+        kinds = (C.c_int * n)(*[KIND[r[1]] for r in rows])
+        progs = (C.c_char_p * n)(*[(r[2] or "").encode() for r in rows])
+        err = C.create_string_buffer(8192)
+        h = lib().orc_net_load(n, names, kinds, progs, master[0].encode() if master else None, err, len(err))
+        if not h:
+            raise OracleParseError(err.value.decode(errors="surrogateescape"))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_net_free(self._h)
+            self._h = None
+
+    def compute_batch(self, values, *, budget: Optional[int] = None, stack_cap: Optional[int] = None,
+                      stop_on_output: bool = False, threads: int = 1):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        n = v.size
+        out = np.zeros(n, np.int32)
+        st = np.zeros(n, np.uint8)
+        sp = np.zeros(n, np.uint32)
+        rc = lib().orc_compute_batch(
+            self._h,
+            v.ctypes.data_as(C.c_void_p),
+            n,
+            out.ctypes.data_as(C.c_void_p),
+            st.ctypes.data_as(C.c_void_p),
+            sp.ctypes.data_as(C.c_void_p),
+            budget or (1 << 20),
+            1024 if stack_cap is None else stack_cap,
+            1 if stop_on_output else 0,
+            threads,
+        )
+        assert rc == 0
+        return out, st, sp
+
+
+def gen_inputs(seed: int, n: int, *, kind: int = 0, mask: int = 0, offset: int = 0) -> np.ndarray:
+    out = np.zeros(n, np.int64)
+    lib().orc_gen_inputs(seed, kind, mask, offset, n, out.ctypes.data_as(C.c_void_p))
+    return out

@@ -1,0 +1,51 @@
+"""The C-ABI library loads without a GPU and exports every entry point that
+include/mk.h declares; the product path refuses to run without its library."""
+import ctypes
+import os
+import re
+
+import misaka_net_amd as mk
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    text = open(os.path.join(ROOT, "include", "mk.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mk_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    names = declared_functions()
+    for required in ["mk_net_load", "mk_net_free", "mk_compute_batch", "mk_compute_device"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(mk._native.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(declared_functions()) <= set(mk._native.SIGNATURES)
+
+
+def test_library_is_gfx950_code_object():
+    data = open(mk._native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version():
+    assert b"gfx950" in mk._native.lib().mk_version()
+
+
+def test_compute_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        return
+    net = mk.Network(mk.networks.example_network())
+    try:
+        net.compute_batch([1, 2, 3])
+    except mk._native.MkError as e:
+        assert e.code == mk._native.MK_EDEVICE
+    else:
+        raise AssertionError("compute_batch must not succeed without a GPU")

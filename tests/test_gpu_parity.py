@@ -1,0 +1,202 @@
+"""GPU executor (HIP, via the C ABI) against the CPU oracle: bit-exact
+out/status/steps on seeded inputs, plus size-independent properties at the
+BASELINE.json sizes."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import misaka_net_amd as mk
+from misaka_net_amd import _native as N
+from oracle import pyoracle as po
+from tisgen import random_network
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x4D49534B41
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def oracle(nodes, xs, **kw):
+    return po.OracleNet(nodes).compute_batch(xs, threads=THREADS, **kw)
+
+
+def assert_same(got, ref, ctx=""):
+    out, st, sp = ref
+    bad = np.nonzero((got.out != out) | (got.status != st) | (got.steps != sp))[0]
+    if bad.size:
+        i = int(bad[0])
+        raise AssertionError(
+            f"{ctx}: {bad.size} lanes differ; lane {i}: gpu (out={got.out[i]}, st={got.status[i]:#x}, "
+            f"steps={got.steps[i]}) oracle (out={out[i]}, st={st[i]:#x}, steps={sp[i]})"
+        )
+
+
+def test_readme_kat_on_gpu(gpu):
+    net = mk.Network(mk.networks.example_network())
+    r = net.compute_batch([5, 0, -7, 2147483646, 2147483647, -2147483648, 4294967301, -4294967296])
+    assert r.out.tolist() == [7, 2, -5, -2147483648, -2147483647, -2147483646, 7, 2]
+    assert (r.status == 0x11).all() and (r.steps == 12).all()
+
+
+@pytest.mark.parametrize(
+    "name,nodes,n,gen",
+    [
+        ("c2_example", mk.networks.example_network(), 1 << 17, (N.MK_GEN_FULL, 0)),
+        ("c3_sample", mk.networks.sample_network(), 1 << 17, (N.MK_GEN_FULL, 0)),
+        ("c4_pipeline_d64", mk.networks.pipeline_network(64), 1 << 12, (N.MK_GEN_FULL, 0)),
+        ("c5_countdown", mk.networks.countdown_network(), 1 << 15, (N.MK_GEN_MASKED, 1023)),
+    ],
+)
+def test_configs_bit_exact(gpu, name, nodes, n, gen):
+    xs = po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1])
+    got = mk.Network(nodes).compute_batch(xs)
+    assert_same(got, oracle(nodes, xs), name)
+
+
+def test_c4_deep_stacks_spill_to_hbm(gpu):
+    nodes = mk.networks.pipeline_network(1024)
+    xs = po.gen_inputs(SEED, 600)
+    got = mk.Network(nodes).compute_batch(xs)
+    ref = oracle(nodes, xs)
+    assert_same(got, ref, "c4 D=1024")
+    assert (got.status == 0x11).all()
+
+
+def test_c5_zero_trip_and_maximum_trip(gpu):
+    nodes = mk.networks.countdown_network()
+    xs = np.arange(0, 1024, dtype=np.int64)
+    assert_same(mk.Network(nodes).compute_batch(xs), oracle(nodes, xs), "c5 all trip counts")
+
+
+@pytest.mark.parametrize("seed", range(0, 240, 1))
+def test_random_networks_bit_exact(gpu, seed):
+    rows = random_network(seed)
+    xs = po.gen_inputs(seed * 7919 + 1, 256)
+    cap = [1, 3, 8, 16, 17, 40, 1024][seed % 7]
+    kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=cap, stop_on_output=(seed % 5 == 4))
+    got = mk.Network(rows).compute_batch(xs, **kw)
+    assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
+
+
+def test_budget_and_stop_on_output(gpu):
+    nodes = [("a", "program", "JRO 0"), ("b", "program", "OUT 3\nJRO 0")]
+    got = mk.Network(nodes).compute_batch([0] * 70, budget=11)
+    assert (got.steps == 12).all() and (got.status == (N.MK_ST_BUDGET | N.MK_ST_HAS_OUTPUT)).all()
+    got = mk.Network(nodes).compute_batch([0] * 70, stop_on_output=True)
+    assert (got.steps == 2).all() and (got.status == (N.MK_ST_OUTPUT_STOP | N.MK_ST_HAS_OUTPUT)).all()
+
+
+def test_empty_batch(gpu):
+    got = mk.Network(mk.networks.example_network()).compute_batch([])
+    assert got.out.size == 0
+
+
+def test_ragged_sizes(gpu):
+    nodes = mk.networks.sample_network()
+    net = mk.Network(nodes)
+    for n in [1, 63, 64, 65, 255, 257, 1000, 4097]:
+        xs = po.gen_inputs(n, n)
+        assert_same(net.compute_batch(xs), oracle(nodes, xs), f"n={n}")
+
+
+def test_concurrent_host_calls(gpu):
+    nodes = mk.networks.example_network()
+    net = mk.Network(nodes)
+    xs = [po.gen_inputs(s, 50000) for s in range(4)]
+    res = [None] * 4
+
+    def work(i):
+        res[i] = net.compute_batch(xs[i])
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for i in range(4):
+        assert_same(res[i], oracle(nodes, xs[i]), f"thread {i}")
+
+
+def test_device_generator_matches_oracle(gpu):
+    import torch
+
+    n = 1 << 20
+    d = torch.empty(n, dtype=torch.int32, device="cuda")
+    mk.generate_inputs_device(n, d.data_ptr(), seed=SEED, offset=12345,
+                              stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), po.gen_inputs(SEED, n, offset=12345).astype(np.int32))
+
+
+def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FULL, 0), offset=0):
+    import torch
+
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sp = torch.empty(n, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+    net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), steps_ptr=sp.data_ptr(),
+                       stats_ptr=stats.data_ptr(), in_ptr=None if in_tensor is None else in_tensor.data_ptr(),
+                       in_kind=in_kind, seed=SEED, gen_kind=gen[0], gen_mask=gen[1], offset=offset,
+                       stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), st.cpu().numpy(), sp.cpu().numpy().view(np.uint32), stats.cpu().numpy()
+
+
+def test_device_api_input_kinds_agree(gpu):
+    import torch
+
+    nodes = mk.networks.sample_network()
+    net = mk.Network(nodes)
+    n = 100003
+    x64 = po.gen_inputs(SEED, n, offset=777)
+    a = _device_run(net, n, offset=777)
+    b = _device_run(net, n, in_tensor=torch.from_numpy(x64.astype(np.int32)).cuda(), in_kind=N.MK_IN_I32)
+    c = _device_run(net, n, in_tensor=torch.from_numpy(x64).cuda(), in_kind=N.MK_IN_I64)
+    ref = oracle(nodes, x64)
+    for r in (a, b, c):
+        for u, v in zip(r[:3], ref):
+            assert np.array_equal(u, v)
+        assert r[3][0] == int(ref[2].sum()) and r[3][2] == n
+        assert r[3][1] == int(((ref[1] & 0x10) != 0).sum())
+
+
+def test_c2_full_size_properties(gpu):
+    # BASELINE config 2: 16,777,216 lanes; size-independent checks:
+    # out == int32(x + 2) (README.md:39-44), 12 retired instrs, quiescent + output.
+    import torch
+
+    n = 1 << 24
+    net = mk.Network(mk.networks.example_network())
+    x = torch.empty(n, dtype=torch.int32, device="cuda")
+    mk.generate_inputs_device(n, x.data_ptr(), seed=SEED, stream=torch.cuda.current_stream().cuda_stream)
+    out, st, sp, stats = _device_run(net, n, in_tensor=x)
+    xe = x.cpu().numpy().astype(np.int64)
+    assert np.array_equal(out, ((xe + 2 + 2**31) % 2**32 - 2**31).astype(np.int32))
+    assert (st == 0x11).all() and (sp == 12).all()
+    assert stats[0] == 12 * n and stats[1] == n and stats[2] == n and stats[3] == n
+    # a seeded slice bit-exact against the oracle, edge lanes included
+    sl = slice(n - 4096, n)
+    ref = oracle(mk.networks.example_network(), xe[sl])
+    assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
+
+
+def test_c3_64m_shard_properties(gpu):
+    # BASELINE config 3 shards 67,108,864 lanes over 8 GPUs; one shard here
+    # (lanes [7*8M, 8*8M)) with the global lane offset of rank 7.
+    n = 1 << 23
+    off = 7 * n
+    nodes = mk.networks.sample_network()
+    net = mk.Network(nodes)
+    out, st, sp, stats = _device_run(net, n, offset=off)
+    x = po.gen_inputs(SEED, n, offset=off)
+    x32 = x.astype(np.int32).astype(np.int64)
+    want = ((2 * x32 + 2**31) % 2**32 - 2**31).astype(np.int32)
+    nz = x32 != 0
+    assert np.array_equal(out[nz], want[nz]) and (out[~nz] == 0).all()
+    assert (st[nz] == 0x11).all() and (st[~nz] == N.MK_ST_QUIESCENT).all()
+    # steps depend only on the sign class; pin each class with the oracle
+    for cls in (x32 > 0, x32 < 0, x32 == 0):
+        if cls.any():
+            i = int(np.nonzero(cls)[0][0])
+            assert (sp[cls] == oracle(nodes, x[i:i + 1])[2][0]).all()
