@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per GPU (default: the config's)")
     ap.add_argument("--gather", action="store_true", help="also time an ordered RCCL gather of outputs to rank 0")
+    ap.add_argument("--interp", action="store_true", help="force the tier-1 bytecode interpreter")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -140,7 +141,7 @@ def main():
 
     def step(stats_ptr):
         net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats_ptr,
-                           in_ptr=x.data_ptr(), in_kind=N.MK_IN_I32, device=dev, stream=sh)
+                           in_ptr=x.data_ptr(), in_kind=N.MK_IN_I32, device=dev, stream=sh, interp=args.interp)
 
     for _ in range(args.warmup):
         step(None)
@@ -221,6 +222,7 @@ def main():
                 "global_lanes": lanes * world,
                 "network": args.config,
                 "parallelism": f"dp{world} (contiguous lane shards, no data-path collective)",
+                "executor": net.plan(interp=args.interp),
             },
             "results_per_s": with_out / wall_max,
             "node_instr_per_lane": retired / (lanes * world * args.steps),

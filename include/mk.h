@@ -61,6 +61,11 @@ typedef struct {
 } mk_node_desc;
 
 #define MK_FLAG_STOP_ON_OUTPUT 1u
+/* Skip the schedule compiler and run the direct bytecode interpreter
+ * (tier 1).  By default a network is first compiled into superblocks of
+ * micro-ops (tier 2); networks the compiler cannot bound fall back to
+ * tier 1 automatically.  Both tiers give identical results. */
+#define MK_FLAG_FORCE_INTERP 2u
 
 typedef struct {
     uint32_t budget;      /* retired node-instructions per lane; 0 = 1<<20          */
@@ -132,6 +137,15 @@ int mk_tokenize(const char *program, char *out, size_t out_len);
 
 /* Lowered bytecode of a loaded network as text (one instruction per line). */
 int mk_net_disasm(const mk_net *net, char *out, size_t out_len);
+
+/* Which tier `opts` selects for this network and its shape, as one line of
+ * text ("tier=compiled superblocks=.. regs=.. words=.." or
+ * "tier=interp reason=.."); compiles the schedule if not cached yet. */
+int mk_net_plan(mk_net *net, const mk_opts *opts, char *out, size_t out_len);
+
+/* Micro-op listing of the compiled schedule for `opts` (MK_ELIMIT if the
+ * network is not compilable). */
+int mk_net_sched_disasm(mk_net *net, const mk_opts *opts, char *out, size_t out_len);
 
 /* counts: [0] program nodes [1] stack nodes [2] total instructions */
 int mk_net_info(const mk_net *net, int *counts3);

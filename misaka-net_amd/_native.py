@@ -33,6 +33,7 @@ MK_NODE_STACK = 1
 MK_NODE_MASTER = 2
 
 MK_FLAG_STOP_ON_OUTPUT = 1
+MK_FLAG_FORCE_INTERP = 2
 
 MK_IN_I64 = 0
 MK_IN_I32 = 1
@@ -104,6 +105,8 @@ SIGNATURES = {
     "mk_tokenize": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "mk_net_disasm": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "mk_net_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    "mk_net_plan": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
+    "mk_net_sched_disasm": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
     "mk_valu_probe_device": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
     "mk_version": (C.c_char_p, []),
 }

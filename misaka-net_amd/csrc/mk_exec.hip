@@ -28,12 +28,14 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/mk.h"
 #include "tis_front.h"
+#include "tis_sched.h"
 
 namespace mk {
 
@@ -338,6 +340,197 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
     }
 }
 
+// ------------------------------------------------------------------------
+// Tier 2: superblock executor for a compiled schedule (tis_sched.cpp).
+//
+// Each lane carries only its superblock id, its retired-instruction count
+// and a small file of 64-bit registers in LDS ([reg][lane], conflict-free
+// for every access); stack entries that outlive a superblock sit in HBM
+// slots laid out [slot][lane] (coalesced).  A wave picks the superblock of
+// its lowest active lane, runs the lanes that share it through the
+// micro-op stream (scalar fetch + scalar dispatch, VALU only for the data),
+// and repeats; lanes leave a superblock at BR/JRO/JUMP/END/GUARD/ROUND_END.
+// ------------------------------------------------------------------------
+struct SParams {
+    int in_kind;
+    uint32_t gen_kind;
+    const void *in_data;
+    uint64_t seed;
+    uint64_t offset;
+    uint32_t gen_mask;
+    uint32_t budget;
+    uint64_t n;
+    int32_t *out;
+    uint8_t *status;
+    uint32_t *steps;
+    unsigned long long *stats;
+    int32_t *slots;   // [nslots][lanes]
+    uint64_t lanes;   // resident lanes
+    uint32_t in_reg;
+};
+
+__device__ __forceinline__ UOp fetch_uop(const UOp *__restrict__ code, uint32_t i)
+{
+    const uint4 w = reinterpret_cast<const uint4 *>(code)[i];
+    UOp u;
+    u.op = (uint8_t)(w.x & 0xffu);
+    u.fl = (uint8_t)((w.x >> 8) & 0xffu);
+    u.d = (uint16_t)(w.x >> 16);
+    u.a = (uint16_t)(w.y & 0xffffu);
+    u.b = (uint16_t)(w.y >> 16);
+    u.imm = (int64_t)(((uint64_t)w.w << 32) | (uint64_t)w.z);
+    return u;
+}
+
+__device__ __forceinline__ int32_t sched_input(const SParams &p, uint64_t i)
+{
+    if (p.in_kind == MK_IN_I64) return (int32_t)((const int64_t *)p.in_data)[i];
+    if (p.in_kind == MK_IN_I32) return ((const int32_t *)p.in_data)[i];
+    return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
+}
+
+__global__ void __launch_bounds__(kBlock) tis_sched_exec(const UOp *__restrict__ code,
+                                                         const uint32_t *__restrict__ entry,
+                                                         const uint32_t *__restrict__ jtab, SParams p)
+{
+    extern __shared__ int64_t R[]; // [nregs][blockDim.x]
+    const uint32_t B = blockDim.x;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
+    auto reg = [&](uint32_t r) -> int64_t & { return R[r * B + tid]; };
+    auto opnd = [&](uint32_t r, bool t) -> int64_t {
+        const int64_t v = reg(r);
+        return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v;
+    };
+
+    unsigned long long s_steps = 0, s_out = 0, s_done = 0, s_q = 0, s_b = 0, s_ov = 0, s_os = 0;
+    uint64_t idx = gid;
+    bool active = idx < p.n;
+    uint32_t sb = 0, steps = 0;
+    if (active) reg(p.in_reg) = sched_input(p, idx);
+
+    for (;;) {
+        const unsigned long long act = __ballot(active);
+        if (!act) break;
+        const int lead = __builtin_ctzll(act);
+        const uint32_t u = __builtin_amdgcn_readlane(sb, lead);
+        if (!(active && sb == u)) continue;
+        uint32_t pc = entry[u]; // wave-uniform
+        bool done = false;
+        uint32_t st = 0;
+        int32_t outv = 0;
+        for (;;) {
+            const UOp I = fetch_uop(code, pc);
+            bool leave = false;
+            switch (I.op) {
+            case U_MOV: reg(I.d) = opnd(I.a, I.fl & UF_TA); pc += 1; break;
+            case U_LI: reg(I.d) = I.imm; pc += 1; break;
+            case U_ADD:
+                reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) + (uint64_t)opnd(I.b, I.fl & UF_TB));
+                pc += 1;
+                break;
+            case U_SUB:
+                reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) - (uint64_t)opnd(I.b, I.fl & UF_TB));
+                pc += 1;
+                break;
+            case U_ADDI: reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) + (uint64_t)I.imm); pc += 1; break;
+            case U_RSUBI: reg(I.d) = (int64_t)((uint64_t)I.imm - (uint64_t)opnd(I.a, I.fl & UF_TA)); pc += 1; break;
+            case U_ST: p.slots[(uint64_t)I.imm * p.lanes + gid] = (int32_t)opnd(I.a, I.fl & UF_TA); pc += 1; break;
+            case U_STI:
+                p.slots[(uint64_t)((uint32_t)I.a | ((uint32_t)I.b << 16)) * p.lanes + gid] = (int32_t)I.imm;
+                pc += 1;
+                break;
+            case U_LD: reg(I.d) = p.slots[(uint64_t)I.imm * p.lanes + gid]; pc += 1; break;
+            case U_JUMP:
+                steps += (uint32_t)I.d | ((uint32_t)I.a << 16);
+                sb = (uint32_t)I.imm;
+                leave = true;
+                break;
+            case U_BR: {
+                const int64_t v = opnd(I.a, I.fl & UF_TA);
+                const uint32_t cond = (I.fl >> UF_COND_SHIFT) & 3u;
+                const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
+                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
+                sb = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
+                leave = true;
+                break;
+            }
+            case U_JRO: {
+                // IntClamp(ptr+v, 0, len-1) with an int64 wrapping add (program.go:354,362)
+                int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)opnd(I.a, I.fl & UF_TA));
+                t = t > (int64_t)I.b ? (int64_t)I.b : t;
+                t = t < 0 ? 0 : t;
+                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
+                sb = jtab[(uint64_t)I.imm + (uint64_t)t];
+                leave = true;
+                break;
+            }
+            case U_END:
+                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
+                outv = (I.fl & UF_OUTREG) ? (int32_t)opnd(I.a, I.fl & UF_TA) : (int32_t)I.imm;
+                st = I.d;
+                done = true;
+                leave = true;
+                break;
+            case U_GUARD:
+                if ((uint64_t)steps + ((uint32_t)I.d | ((uint32_t)I.a << 16)) >= p.budget) {
+                    sb = (uint32_t)I.imm; // budget may be hit inside: take the checked variant
+                    leave = true;
+                }
+                pc += 1;
+                break;
+            case U_ROUND_END: {
+                const uint32_t c = (uint32_t)fetch_uop(code, pc + 1).imm;
+                if ((uint64_t)steps + c >= p.budget) {
+                    steps += c;
+                    outv = (I.fl & UF_OUTREG) ? (int32_t)opnd(I.a, I.fl & UF_TA) : (int32_t)I.imm;
+                    st = I.d;
+                    done = true;
+                    leave = true;
+                }
+                pc += 2;
+                break;
+            }
+            default: leave = true; done = true; st = 0; break; // corrupt stream: stop the lane
+            }
+            if (leave) break;
+        }
+        if (done) {
+            const uint32_t reason = st & MK_ST_REASON_MASK;
+            p.out[idx] = (st & MK_ST_HAS_OUTPUT) ? outv : 0;
+            p.status[idx] = (uint8_t)st;
+            if (p.steps) p.steps[idx] = steps;
+            s_steps += steps;
+            s_out += (st & MK_ST_HAS_OUTPUT) != 0;
+            s_done += 1;
+            s_q += reason == MK_ST_QUIESCENT;
+            s_b += reason == MK_ST_BUDGET;
+            s_ov += reason == MK_ST_STACK_OVERFLOW;
+            s_os += reason == MK_ST_OUTPUT_STOP;
+            idx += p.lanes;
+            active = idx < p.n;
+            sb = 0;
+            steps = 0;
+            if (active) reg(p.in_reg) = sched_input(p, idx);
+        }
+    }
+
+    if (p.stats) {
+        const unsigned long long v0 = wave_sum(s_steps), v1 = wave_sum(s_out), v2 = wave_sum(s_done),
+                                 v3 = wave_sum(s_q), v4 = wave_sum(s_b), v5 = wave_sum(s_ov),
+                                 v6 = wave_sum(s_os);
+        if ((tid & 63) == 0 && v2) {
+            atomicAdd(&p.stats[0], v0);
+            atomicAdd(&p.stats[1], v1);
+            atomicAdd(&p.stats[2], v2);
+            if (v3) atomicAdd(&p.stats[3], v3);
+            if (v4) atomicAdd(&p.stats[4], v4);
+            if (v5) atomicAdd(&p.stats[5], v5);
+            if (v6) atomicAdd(&p.stats[6], v6);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
                                                      uint64_t offset, uint64_t n, int32_t *out)
 {
@@ -373,6 +566,24 @@ __global__ void __launch_bounds__(kBlock) valu_probe(int iters, uint32_t *sink)
 // ------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------
+struct SchedDev {
+    UOp *d_code = nullptr;
+    uint32_t *d_entry = nullptr;
+    uint32_t *d_jtab = nullptr;
+    int32_t *d_slots = nullptr;
+    size_t slots_bytes = 0;
+};
+
+// A compiled schedule for one (stack_cap, stop_on_output) pair.
+struct SchedCache {
+    uint32_t cap = 0;
+    bool soo = false;
+    bool ok = false;
+    std::string why;
+    SchedProgram prog;
+    SchedDev dev[kMaxDevices];
+};
+
 struct DevCtx {
     bool ready = false;
     Insn *d_code = nullptr;
@@ -388,8 +599,9 @@ struct DevCtx {
 
 struct mk_net {
     mk::Network net;
-    std::mutex mu;      // serialises host-API calls and device-context setup
+    std::mutex mu;      // serialises host-API calls, compilation and device-context setup
     mk::DevCtx dev[mk::kMaxDevices];
+    std::vector<std::unique_ptr<mk::SchedCache>> sched;
     ~mk_net()
     {
         int prev = 0;
@@ -402,6 +614,12 @@ struct mk_net {
             (void)hipFree(c.d_code);
             (void)hipFree(c.d_spill);
             (void)hipFree(c.d_stage);
+            for (auto &sc : sched) {
+                (void)hipFree(sc->dev[d].d_code);
+                (void)hipFree(sc->dev[d].d_entry);
+                (void)hipFree(sc->dev[d].d_jtab);
+                (void)hipFree(sc->dev[d].d_slots);
+            }
             if (c.stream) (void)hipStreamDestroy(c.stream);
         }
         (void)hipSetDevice(prev);
@@ -501,6 +719,96 @@ void resolve_opts(const mk_opts *o, uint32_t &budget, uint32_t &cap, uint32_t &f
     flags = o ? o->flags : 0u;
 }
 
+// Caller holds h->mu.  Compiles the schedule for (cap, soo) once.
+SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
+{
+    for (auto &sc : h->sched)
+        if (sc->cap == cap && sc->soo == soo) return sc.get();
+    auto sc = std::make_unique<SchedCache>();
+    sc->cap = cap;
+    sc->soo = soo;
+    SchedLimits lim;
+    sc->ok = compile_schedule(h->net, cap, soo, lim, sc->prog, sc->why);
+    h->sched.push_back(std::move(sc));
+    return h->sched.back().get();
+}
+
+// Caller holds h->mu.
+int ensure_sched_device(SchedCache *sc, int d)
+{
+    SchedDev &sd = sc->dev[d];
+    if (sd.d_code) return MK_OK;
+    DeviceGuard g(d);
+    const SchedProgram &P = sc->prog;
+    const size_t cb = P.code.size() * sizeof(UOp), eb = P.entry.size() * 4, jb = std::max<size_t>(P.jtab.size(), 1) * 4;
+    if (hipMalloc(&sd.d_code, cb) != hipSuccess || hipMalloc(&sd.d_entry, eb) != hipSuccess ||
+        hipMalloc(&sd.d_jtab, jb) != hipSuccess)
+        return MK_ENOMEM;
+    if (hipMemcpy(sd.d_code, P.code.data(), cb, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(sd.d_entry, P.entry.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
+        (!P.jtab.empty() && hipMemcpy(sd.d_jtab, P.jtab.data(), P.jtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return MK_EDEVICE;
+    return MK_OK;
+}
+
+// Caller holds h->mu.  Tier-2 launch; asynchronous on `stream`.
+int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
+                        uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, hipStream_t stream)
+{
+    int rc = ensure_sched_device(sc, d);
+    if (rc) return rc;
+    DevCtx &c = h->dev[d];
+    SchedDev &sd = sc->dev[d];
+    const SchedProgram &P = sc->prog;
+    DeviceGuard g(d);
+    // LDS register file: nregs x 8 B per lane; keep <= 40 KiB per block.
+    int B = 256;
+    while (B > 64 && (size_t)P.nregs * B * 8 > 40 * 1024) B >>= 1;
+    const size_t lds = (size_t)P.nregs * B * 8;
+    if (lds > 160 * 1024) return MK_ELIMIT;
+    void *fn = reinterpret_cast<void *>(&tis_sched_exec);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const uint64_t want = (n + B - 1) / B;
+    const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(c.cus, 1);
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    const uint64_t lanes = (uint64_t)blocks * B;
+    if (P.nslots) {
+        const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
+        if (need > sd.slots_bytes) {
+            if (sd.d_slots) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(sd.d_slots);
+                sd.d_slots = nullptr;
+                sd.slots_bytes = 0;
+            }
+            if (hipMalloc(&sd.d_slots, need) != hipSuccess) return MK_ENOMEM;
+            sd.slots_bytes = need;
+        }
+    }
+    SParams p{};
+    p.in_kind = in->kind;
+    p.gen_kind = in->gen_kind;
+    p.in_data = in->data;
+    p.seed = in->seed;
+    p.offset = in->offset;
+    p.gen_mask = in->gen_mask;
+    p.budget = budget;
+    p.n = n;
+    p.out = d_out;
+    p.status = d_status;
+    p.steps = d_steps;
+    p.stats = reinterpret_cast<unsigned long long *>(d_stats);
+    p.slots = sd.d_slots;
+    p.lanes = lanes;
+    p.in_reg = P.in_reg;
+    const UOp *code = sd.d_code;
+    const uint32_t *entry = sd.d_entry, *jtab = sd.d_jtab;
+    void *args[] = {(void *)&code, (void *)&entry, (void *)&jtab, (void *)&p};
+    if (hipLaunchKernel(fn, dim3(blocks), dim3(B), args, lds, stream) != hipSuccess) return MK_EDEVICE;
+    return MK_OK;
+}
+
 // Caller holds h->mu.  Asynchronous on `stream`.
 int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,
                   uint32_t *d_steps, uint64_t *d_stats, const mk_opts *o, hipStream_t stream)
@@ -512,6 +820,10 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     DeviceGuard g(d);
     uint32_t budget, cap, flags;
     resolve_opts(o, budget, cap, flags);
+    if (!(flags & MK_FLAG_FORCE_INTERP)) {
+        SchedCache *sc = get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
+        if (sc->ok) return launch_sched_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, stream);
+    }
     Launch L;
     if ((rc = plan_launch(h->net, c, n, cap, L))) return rc;
     const uint64_t lanes = (uint64_t)L.blocks * kBlock;
@@ -751,6 +1063,38 @@ int mk_net_disasm(const mk_net *net, char *out, size_t out_len)
 {
     if (!net) return MK_EINVAL;
     return mk::copy_out(out, out_len, mk::disasm(net->net));
+}
+
+int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
+{
+    if (!h) return MK_EINVAL;
+    uint32_t budget, cap, flags;
+    mk::resolve_opts(opts, budget, cap, flags);
+    char buf[512];
+    if (flags & MK_FLAG_FORCE_INTERP) {
+        snprintf(buf, sizeof buf, "tier=interp reason=forced");
+        return mk::copy_out(out, out_len, buf);
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    mk::SchedCache *sc = mk::get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
+    if (sc->ok)
+        snprintf(buf, sizeof buf, "tier=compiled superblocks=%u regs=%u slots=%u words=%zu jtab=%zu rounds=%llu",
+                 sc->prog.nsb, sc->prog.nregs, sc->prog.nslots, sc->prog.code.size(), sc->prog.jtab.size(),
+                 (unsigned long long)sc->prog.sym_rounds);
+    else
+        snprintf(buf, sizeof buf, "tier=interp reason=%s", sc->why.c_str());
+    return mk::copy_out(out, out_len, buf);
+}
+
+int mk_net_sched_disasm(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
+{
+    if (!h) return MK_EINVAL;
+    uint32_t budget, cap, flags;
+    mk::resolve_opts(opts, budget, cap, flags);
+    std::lock_guard<std::mutex> lk(h->mu);
+    mk::SchedCache *sc = mk::get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
+    if (!sc->ok) return MK_ELIMIT;
+    return mk::copy_out(out, out_len, mk::sched_disasm(sc->prog));
 }
 
 int mk_net_info(const mk_net *net, int *counts3)

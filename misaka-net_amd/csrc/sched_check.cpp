@@ -1,0 +1,145 @@
+// sched_check.cpp -- host model of the tier-2 superblock executor
+// (tis_sched_exec in mk_exec.hip), built into a separate CHECK library
+// (lib/libmisaka_amd_check.so) so the schedule compiler can be fuzzed against
+// the CPU oracle without a GPU.  It is not part of the product library and
+// no product entry point can reach it.
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mk.h"
+#include "tis_front.h"
+#include "tis_sched.h"
+
+namespace {
+
+struct CheckNet {
+    mk::Network net;
+};
+
+inline int64_t sx(int64_t v, bool t) { return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v; }
+
+} // namespace
+
+extern "C" {
+
+void *mkc_load(const mk_node_desc *nodes, int n, char *err, size_t err_len)
+{
+    std::vector<mk::NodeSpec> specs;
+    for (int i = 0; i < n; i++) specs.push_back({nodes[i].name, nodes[i].kind, nodes[i].program ? nodes[i].program : ""});
+    auto *h = new CheckNet();
+    std::string e;
+    if (mk::lower_network(specs, h->net, e)) {
+        snprintf(err, err_len, "%s", e.c_str());
+        delete h;
+        return nullptr;
+    }
+    return h;
+}
+
+void mkc_free(void *h) { delete (CheckNet *)h; }
+
+// Returns 0 when compiled and emulated, 1 when the compiler declined (why),
+// negative on error.  plan (nullable) receives the disassembly.
+int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t *in, size_t n, int32_t *out,
+                uint8_t *status, uint32_t *steps_out, char *why, size_t why_len, char *plan, size_t plan_len)
+{
+    auto *h = (CheckNet *)hv;
+    mk::SchedProgram P;
+    std::string w;
+    mk::SchedLimits lim;
+    if (!mk::compile_schedule(h->net, cap, soo != 0, lim, P, w)) {
+        snprintf(why, why_len, "%s", w.c_str());
+        return 1;
+    }
+    if (plan && plan_len) snprintf(plan, plan_len, "%s", mk::sched_disasm(P).c_str());
+    std::vector<int64_t> R(P.nregs);
+    std::unordered_map<uint32_t, int32_t> slots;
+    for (size_t i = 0; i < n; i++) {
+        std::fill(R.begin(), R.end(), (int64_t)0x5A5A5A5A5A5A5A5All); // stale register contents
+        slots.clear();
+        R[P.in_reg] = (int32_t)in[i];
+        uint32_t sb = 0, steps = 0, st = 0;
+        int32_t outv = 0;
+        bool done = false;
+        uint64_t guard_words = 0;
+        while (!done) {
+            uint32_t pc = P.entry[sb];
+            for (;;) {
+                if (++guard_words > (1ull << 34)) return -2; // runaway
+                const mk::UOp &I = P.code[pc];
+                bool leave = false;
+                const bool ta = I.fl & mk::UF_TA, tb = I.fl & mk::UF_TB;
+                switch (I.op) {
+                case mk::U_MOV: R[I.d] = sx(R[I.a], ta); pc++; break;
+                case mk::U_LI: R[I.d] = I.imm; pc++; break;
+                case mk::U_ADD: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) + (uint64_t)sx(R[I.b], tb)); pc++; break;
+                case mk::U_SUB: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) - (uint64_t)sx(R[I.b], tb)); pc++; break;
+                case mk::U_ADDI: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) + (uint64_t)I.imm); pc++; break;
+                case mk::U_RSUBI: R[I.d] = (int64_t)((uint64_t)I.imm - (uint64_t)sx(R[I.a], ta)); pc++; break;
+                case mk::U_ST: slots[(uint32_t)I.imm] = (int32_t)sx(R[I.a], ta); pc++; break;
+                case mk::U_STI: slots[(uint32_t)I.a | ((uint32_t)I.b << 16)] = (int32_t)I.imm; pc++; break;
+                case mk::U_LD: {
+                    auto it = slots.find((uint32_t)I.imm);
+                    if (it == slots.end()) return -3; // load of a slot never stored
+                    R[I.d] = it->second;
+                    pc++;
+                    break;
+                }
+                case mk::U_JUMP: steps += (uint32_t)I.d | ((uint32_t)I.a << 16); sb = (uint32_t)I.imm; leave = true; break;
+                case mk::U_BR: {
+                    const int64_t v = sx(R[I.a], ta);
+                    const uint32_t c = (I.fl >> mk::UF_COND_SHIFT) & 3u;
+                    const bool take = c == 0 ? v == 0 : c == 1 ? v != 0 : c == 2 ? v > 0 : v < 0;
+                    steps += (uint32_t)P.code[pc + 1].imm;
+                    sb = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
+                    leave = true;
+                    break;
+                }
+                case mk::U_JRO: {
+                    int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)sx(R[I.a], ta));
+                    t = t > (int64_t)I.b ? (int64_t)I.b : t;
+                    t = t < 0 ? 0 : t;
+                    steps += (uint32_t)P.code[pc + 1].imm;
+                    sb = P.jtab[(size_t)I.imm + (size_t)t];
+                    leave = true;
+                    break;
+                }
+                case mk::U_END:
+                    steps += (uint32_t)P.code[pc + 1].imm;
+                    outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(R[I.a], ta) : (int32_t)I.imm;
+                    st = I.d;
+                    done = leave = true;
+                    break;
+                case mk::U_GUARD:
+                    if ((uint64_t)steps + ((uint32_t)I.d | ((uint32_t)I.a << 16)) >= budget) {
+                        sb = (uint32_t)I.imm;
+                        leave = true;
+                    }
+                    pc++;
+                    break;
+                case mk::U_ROUND_END: {
+                    const uint32_t c = (uint32_t)P.code[pc + 1].imm;
+                    if ((uint64_t)steps + c >= budget) {
+                        steps += c;
+                        outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(R[I.a], ta) : (int32_t)I.imm;
+                        st = I.d;
+                        done = leave = true;
+                    }
+                    pc += 2;
+                    break;
+                }
+                default: return -4;
+                }
+                if (leave) break;
+            }
+        }
+        out[i] = (st & MK_ST_HAS_OUTPUT) ? outv : 0;
+        status[i] = (uint8_t)st;
+        if (steps_out) steps_out[i] = steps;
+    }
+    return 0;
+}
+
+} // extern "C"

@@ -1,0 +1,1012 @@
+// tis_sched.cpp -- schedule compiler (see tis_sched.h).
+//
+// The symbolic executor below restates the same update() semantics as the
+// GPU interpreter in mk_exec.hip (program.go:219-566, stack.go:95-155,
+// master.go:233-249) over abstract values:
+//   DEAD   value can never be read again (liveness) -- not part of the state
+//   CONST  compile-time constant (int64; int32-range for 32-bit locations)
+//   REG    lives in a per-lane 64-bit register r (read as sext32 if `tr`)
+//   MEM    a stack entry stored in its lane-major HBM slot
+// Control is concrete.  A superblock ends where control depends on data
+// (conditional jump / JRO on a non-constant), at termination, or where the
+// state at a round end was already compiled (loops merge there).  At every
+// exit the live symbolic values are moved into fixed per-location "home"
+// registers so that all paths into a state agree on where values are.
+#include "tis_sched.h"
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "../../include/mk.h"
+
+namespace mk {
+namespace {
+
+constexpr uint8_t K_DEAD = 0, K_CONST = 1, K_REG = 2, K_MEM = 3;
+
+struct Val {
+    uint8_t kind = K_DEAD;
+    bool tr = false;
+    uint16_t r = 0;
+    int64_t c = 0;
+};
+
+inline Val vconst(int64_t c) { Val v; v.kind = K_CONST; v.c = c; return v; }
+inline Val vdead() { return Val(); }
+inline int64_t sext32(int64_t v) { return (int64_t)(int32_t)(uint32_t)(uint64_t)v; }
+inline int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+inline uint64_t mix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Ctl {
+    std::vector<uint16_t> ip;
+    uint32_t pend = 0, hung = 0;
+    uint64_t pfull = 0;
+    std::vector<uint32_t> depth;
+    bool in_avail = true;
+    uint8_t out_cnt = 0;
+    uint8_t pos = 0;
+    bool changed = false;
+};
+
+struct StackDigest {
+    uint64_t h1 = 0, h2 = 0;
+};
+
+inline void digest_entry(StackDigest &g, uint32_t d, const Val &v, bool add)
+{
+    const uint64_t k = (v.kind == K_CONST) ? (uint64_t)v.c : 0x5359'4D42'4F4C'4943ull; // "SYMBOLIC"
+    const uint64_t a = mix64(((uint64_t)d << 2) ^ (v.kind == K_CONST ? 1 : 2) ^ mix64(k));
+    const uint64_t b = mix64(a ^ 0xA5A5'5A5A'C3C3'3C3Cull);
+    if (add) { g.h1 += a; g.h2 += b; }
+    else { g.h1 -= a; g.h2 -= b; }
+}
+
+struct EntryState {
+    Ctl ctl;
+    std::vector<Val> loc;               // K_DEAD / K_CONST / K_REG(home) -- REG means "in home"
+    std::vector<std::vector<Val>> stk;  // K_CONST / K_MEM
+    std::vector<StackDigest> dig;
+};
+
+enum { A_CONT = 0, A_EXIT = 1 };
+
+class Compiler {
+  public:
+    Compiler(const Network &net, uint32_t cap, bool soo, const SchedLimits &lim)
+        : net_(net), cap_(cap), soo_(soo), lim_(lim), N_(net.nprog), S_(net.uses_stacks ? net.nstack : 0)
+    {
+        L0_ = 7 * N_ + 2;
+        home_.assign(L0_, -1);
+    }
+
+    bool run(SchedProgram &out, std::string &why);
+
+  private:
+    // ---- location space -------------------------------------------------
+    int ACC(int n) const { return n; }
+    int BAK(int n) const { return N_ + n; }
+    int PORT(int slot) const { return 2 * N_ + slot; }
+    int PENDV(int n) const { return 6 * N_ + n; }
+    int INL() const { return 7 * N_; }
+    int OUTL() const { return 7 * N_ + 1; }
+    bool is32(int loc) const { return loc >= 2 * N_; }
+
+    const Network &net_;
+    uint32_t cap_;
+    bool soo_;
+    SchedLimits lim_;
+    int N_, S_, L0_;
+    std::vector<std::vector<uint8_t>> acc_live_, bak_live_;
+
+    // homes (global, permanent)
+    std::vector<int> home_;
+    std::vector<uint8_t> claimed_; // register is some location's home
+
+    // entries / work list
+    std::vector<EntryState> entries_;
+    std::unordered_map<std::string, uint32_t> memo_;
+    std::deque<uint32_t> work_;
+    std::vector<std::vector<UOp>> sb_code_; // per entry, with ROUND_END markers
+    std::vector<uint32_t> jtab_;
+    uint32_t total_words_ = 0;
+    uint64_t rounds_ = 0;
+    bool fail_ = false;
+    std::string why_;
+
+    // trace state
+    Ctl ctl_;
+    std::vector<Val> loc_;
+    std::vector<std::vector<Val>> stk_;
+    std::vector<StackDigest> dig_;
+    std::vector<int> refcnt_;
+    std::vector<uint8_t> r32_;
+    std::vector<UOp> code_;
+    uint32_t steps_ = 0;
+    uint32_t max_reg_ = 0;
+    uint32_t max_slot_ = 0;
+    bool any_slot_ = false;
+    std::vector<std::vector<int32_t>> slot_id_; // [stack][depth] -> dense HBM slot, -1 = none yet
+
+    uint32_t slot_of(int s, uint32_t d)
+    {
+        if (slot_id_.size() < (size_t)S_) slot_id_.resize(S_);
+        auto &v = slot_id_[s];
+        if (v.size() <= d) v.resize(d + 1, -1);
+        if (v[d] < 0) v[d] = (int32_t)max_slot_++;
+        any_slot_ = true;
+        return (uint32_t)v[d];
+    }
+
+    // ---- helpers --------------------------------------------------------
+    void failf(const std::string &w)
+    {
+        if (!fail_) { fail_ = true; why_ = w; }
+    }
+    void ensure_reg(int r)
+    {
+        if ((size_t)r >= refcnt_.size()) {
+            refcnt_.resize(r + 1, 0);
+            r32_.resize(r + 1, 0);
+            claimed_.resize(r + 1, 0);
+        }
+        if ((uint32_t)r + 1 > max_reg_) max_reg_ = r + 1;
+        if ((uint32_t)r >= lim_.max_regs) failf("register budget exceeded");
+    }
+    void incref(const Val &v)
+    {
+        if (v.kind == K_REG) { ensure_reg(v.r); refcnt_[v.r]++; }
+    }
+    void decref(const Val &v)
+    {
+        if (v.kind == K_REG) refcnt_[v.r]--;
+    }
+    void set_loc(int X, Val v)
+    {
+        incref(v);
+        decref(loc_[X]);
+        loc_[X] = v;
+    }
+    // a value as stored into a 32-bit location (int32() at every hop)
+    Val trunc(const Val &v)
+    {
+        if (v.kind == K_CONST) return vconst(sext32(v.c));
+        if (v.kind == K_REG) {
+            Val w = v;
+            w.tr = !r32_[v.r];
+            return w;
+        }
+        return v;
+    }
+    int fresh_reg(const std::vector<uint8_t> *exclude = nullptr)
+    {
+        for (;;) {
+            int r = 0;
+            for (;; r++) {
+                if ((size_t)r >= refcnt_.size() || (refcnt_[r] == 0 && !(exclude && (size_t)r < exclude->size() && (*exclude)[r])))
+                    break;
+            }
+            if ((uint32_t)r < lim_.soft_regs || !spill_one()) {
+                ensure_reg(r);
+                return r;
+            }
+        }
+    }
+    // Store the oldest register-only stack entry to its HBM slot.
+    bool spill_one()
+    {
+        for (uint32_t d = 0;; d++) {
+            bool any = false;
+            for (int s = 0; s < S_; s++) {
+                if (d >= stk_[s].size()) continue;
+                any = true;
+                Val &v = stk_[s][d];
+                if (v.kind == K_REG && refcnt_[v.r] == 1) {
+                    emit(U_ST, fa(v), 0, v.r, 0, slot_of(s, d));
+                    decref(v);
+                    v = Val();
+                    v.kind = K_MEM; // digest unchanged: still symbolic
+                    return true;
+                }
+            }
+            if (!any) return false;
+        }
+    }
+    void emit(uint8_t op, uint8_t fl, uint32_t d, uint32_t a, uint32_t b, int64_t imm)
+    {
+        UOp u;
+        u.op = op;
+        u.fl = fl;
+        u.d = (uint16_t)d;
+        u.a = (uint16_t)a;
+        u.b = (uint16_t)b;
+        u.imm = imm;
+        code_.push_back(u);
+    }
+    void emit_ext(int64_t imm) { emit(0xFF, 0, 0, 0, 0, imm); }
+    uint8_t fa(const Val &v) const { return v.tr ? UF_TA : 0; }
+    uint8_t fb(const Val &v) const { return v.tr ? UF_TB : 0; }
+
+    // destination register for a new value of location X
+    int dest_for(int X)
+    {
+        const Val &cur = loc_[X];
+        if (cur.kind == K_REG && refcnt_[cur.r] == 1) return cur.r;
+        return fresh_reg();
+    }
+
+    void op_addsub(int X, Val a, Val b, bool sub)
+    {
+        if (a.kind == K_CONST && b.kind == K_CONST) {
+            set_loc(X, vconst(sub ? wsub(a.c, b.c) : wadd(a.c, b.c)));
+            return;
+        }
+        // sources are referenced by locations or by the attempt's hold, so
+        // fresh_reg() cannot hand out their registers
+        const int d = dest_for(X);
+        if (b.kind == K_CONST)
+            emit(U_ADDI, fa(a), d, a.r, 0, sub ? wsub(0, b.c) : b.c);
+        else if (a.kind == K_CONST) {
+            if (sub) emit(U_RSUBI, fa(b), d, b.r, 0, a.c);
+            else emit(U_ADDI, fa(b), d, b.r, 0, a.c);
+        } else {
+            emit(sub ? U_SUB : U_ADD, (uint8_t)(fa(a) | fb(b)), d, a.r, b.r, 0);
+        }
+        Val nv;
+        nv.kind = K_REG;
+        nv.r = (uint16_t)d;
+        set_loc(X, nv);
+        r32_[d] = 0;
+    }
+
+    // ---- liveness of ACC / BAK per node instruction ----------------------
+    void liveness();
+
+    // ---- state management ---------------------------------------------
+    void prune(Ctl &c, std::vector<Val> &loc) const;
+    std::string key_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const;
+    uint32_t get_or_create(const Ctl &c, const std::vector<Val> &loc);
+    void load_entry(uint32_t id);
+
+    // ---- exits ----------------------------------------------------------
+    // Moves every location that is symbolic in any successor into its home
+    // register and stores symbolic stack entries.  `keep` is a value the
+    // exit op still reads afterwards; returns where to read it.
+    Val canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep);
+    void exit_jump();
+    void exit_end(uint8_t reason);
+    void exit_branch(int n, uint8_t cond, uint16_t target);
+    void exit_jro(int n, const Val &v);
+    void round_end_marker();
+    void generalize();
+
+    int attempt(int n);
+    void compile_entry(uint32_t id);
+};
+
+void Compiler::liveness()
+{
+    acc_live_.assign(N_, {});
+    bak_live_.assign(N_, {});
+    for (int n = 0; n < N_; n++) {
+        const uint32_t len = net_.len[n];
+        const Insn *code = &net_.code[net_.base[n]];
+        std::vector<uint8_t> al(len, 0), bl(len, 0);
+        bool changed = true;
+        while (changed) {
+            changed = false;
+            for (int64_t i = (int64_t)len - 1; i >= 0; i--) {
+                const Insn &I = code[i];
+                bool ao = false, bo = false;
+                auto succ = [&](int64_t t) {
+                    ao = ao || al[t];
+                    bo = bo || bl[t];
+                };
+                const int64_t nx = (i + 1 == (int64_t)len) ? 0 : i + 1;
+                switch (I.op) {
+                case OP_JMP: succ(I.arg); break;
+                case OP_JEZ: case OP_JNZ: case OP_JGZ: case OP_JLZ: succ(I.arg); succ(nx); break;
+                case OP_JRO:
+                    if (I.src == SRC_IMM) {
+                        int64_t t = wadd(i, I.imm);
+                        t = std::min<int64_t>(std::max<int64_t>(t, 0), (int64_t)len - 1);
+                        succ(t);
+                    } else {
+                        for (uint32_t t = 0; t < len; t++) succ(t);
+                    }
+                    break;
+                case OP_STUCK: case OP_HANG: case OP_RETRY: break;
+                default: succ(nx); break;
+                }
+                const bool src_acc = I.src == SRC_ACC;
+                bool a = ao, b = bo;
+                switch (I.op) {
+                case OP_NOP: case OP_JMP: case OP_NEG: case OP_ADD: case OP_SUB: break;
+                case OP_JEZ: case OP_JNZ: case OP_JGZ: case OP_JLZ: a = true; break;
+                case OP_SWP: a = bo; b = ao; break;
+                case OP_SAV: a = ao || bo; b = false; break;
+                case OP_MOV: a = I.dst ? (src_acc && ao) : (ao || src_acc); break;
+                case OP_JRO: case OP_SEND: case OP_PUSH: case OP_OUT: a = ao || src_acc; break;
+                case OP_HANG: case OP_RETRY: a = src_acc; b = false; break;
+                case OP_STUCK: a = false; b = false; break;
+                case OP_POP: case OP_IN: if (I.dst) a = false; break;
+                default: break;
+                }
+                if (a != (bool)al[i] || b != (bool)bl[i]) {
+                    al[i] = a;
+                    bl[i] = b;
+                    changed = true;
+                }
+            }
+        }
+        acc_live_[n] = al;
+        bak_live_[n] = bl;
+    }
+}
+
+void Compiler::prune(Ctl &c, std::vector<Val> &loc) const
+{
+    for (int n = 0; n < N_; n++) {
+        const bool h = (c.hung >> n) & 1u;
+        if (h || !acc_live_[n][c.ip[n]]) loc[ACC(n)] = vdead();
+        if (h || !bak_live_[n][c.ip[n]]) loc[BAK(n)] = vdead();
+        if (!((c.pend >> n) & 1u)) loc[PENDV(n)] = vdead();
+    }
+    for (int s = 0; s < 4 * N_; s++)
+        if (!((c.pfull >> s) & 1ull)) loc[PORT(s)] = vdead();
+    if (!c.in_avail) loc[INL()] = vdead();
+}
+
+std::string Compiler::key_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const
+{
+    std::string k;
+    k.reserve(64 + 2 * N_ + 10 * L0_ + 16 * S_);
+    auto put = [&](const void *p, size_t n) { k.append((const char *)p, n); };
+    put(c.ip.data(), c.ip.size() * 2);
+    put(&c.pend, 4);
+    put(&c.hung, 4);
+    put(&c.pfull, 8);
+    put(c.depth.data(), c.depth.size() * 4);
+    const uint8_t misc[4] = {(uint8_t)c.in_avail, c.out_cnt, c.pos, (uint8_t)c.changed};
+    put(misc, 4);
+    for (int X = 0; X < L0_; X++) {
+        const Val &v = loc[X];
+        const uint8_t kd = v.kind == K_MEM ? K_REG : v.kind;
+        k.push_back((char)kd);
+        if (kd == K_CONST) put(&v.c, 8);
+    }
+    for (int s = 0; s < S_; s++) {
+        put(&dig[s].h1, 8);
+        put(&dig[s].h2, 8);
+    }
+    return k;
+}
+
+uint32_t Compiler::get_or_create(const Ctl &c, const std::vector<Val> &loc)
+{
+    const std::string k = key_of(c, loc, dig_);
+    auto it = memo_.find(k);
+    if (it != memo_.end()) return it->second;
+    if (entries_.size() >= lim_.max_superblocks) {
+        failf("superblock budget exceeded");
+        return 0;
+    }
+    EntryState e;
+    e.ctl = c;
+    e.loc.resize(L0_);
+    for (int X = 0; X < L0_; X++) {
+        const Val &v = loc[X];
+        if (v.kind == K_REG || v.kind == K_MEM) {
+            Val h;
+            h.kind = K_REG;
+            h.r = (uint16_t)home_[X];
+            e.loc[X] = h;
+        } else {
+            e.loc[X] = v;
+        }
+    }
+    e.stk.resize(S_);
+    for (int s = 0; s < S_; s++) {
+        e.stk[s].reserve(stk_[s].size());
+        for (const Val &v : stk_[s]) {
+            if (v.kind == K_CONST) e.stk[s].push_back(v);
+            else { Val m; m.kind = K_MEM; e.stk[s].push_back(m); }
+        }
+    }
+    e.dig = dig_;
+    const uint32_t id = (uint32_t)entries_.size();
+    entries_.push_back(std::move(e));
+    memo_.emplace(k, id);
+    work_.push_back(id);
+    return id;
+}
+
+void Compiler::load_entry(uint32_t id)
+{
+    const EntryState &e = entries_[id];
+    ctl_ = e.ctl;
+    std::fill(refcnt_.begin(), refcnt_.end(), 0);
+    std::fill(r32_.begin(), r32_.end(), 0);
+    loc_ = e.loc;
+    for (int X = 0; X < L0_; X++) {
+        if (loc_[X].kind == K_REG) {
+            ensure_reg(loc_[X].r);
+            refcnt_[loc_[X].r]++;
+            r32_[loc_[X].r] = is32(X);
+        }
+    }
+    stk_ = e.stk;
+    dig_ = e.dig;
+    code_.clear();
+    steps_ = 0;
+}
+
+Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep)
+{
+    // 1. which locations must be in their home (symbolic in any successor)
+    std::vector<uint8_t> need(L0_, 0);
+    succ_loc.assign(succ.size(), loc_);
+    for (size_t i = 0; i < succ.size(); i++) {
+        Ctl c = succ[i];
+        prune(c, succ_loc[i]);
+        for (int X = 0; X < L0_; X++)
+            if (succ_loc[i][X].kind == K_REG || succ_loc[i][X].kind == K_MEM) need[X] = 1;
+    }
+    // 2. stack entries: symbolic values go to their HBM slot
+    for (int s = 0; s < S_; s++) {
+        for (uint32_t d = 0; d < (uint32_t)stk_[s].size(); d++) {
+            Val &v = stk_[s][d];
+            if (v.kind == K_REG) {
+                emit(U_ST, fa(v), 0, v.r, 0, slot_of(s, d));
+                decref(v);
+                v = Val();
+                v.kind = K_MEM;
+            }
+        }
+    }
+    // 3. homes
+    for (int X = 0; X < L0_; X++) {
+        if (!need[X] || home_[X] >= 0) continue;
+        const Val &v = loc_[X];
+        if (v.kind == K_REG && !v.tr && !claimed_[v.r]) {
+            // adopt the register the value already lives in ...
+            bool shared = false;
+            for (int Y = 0; Y < L0_ && !shared; Y++)
+                shared = Y != X && need[Y] && home_[Y] < 0 && loc_[Y].kind == K_REG && loc_[Y].r == v.r && Y < X;
+            if (!shared) {
+                home_[X] = v.r;
+                claimed_[v.r] = 1;
+                continue;
+            }
+        }
+        // ... or take a register nobody claims and nothing currently uses
+        for (int r = 0;; r++) {
+            ensure_reg(r);
+            if (fail_) return keep;
+            if (!claimed_[r] && refcnt_[r] == 0) {
+                home_[X] = r;
+                claimed_[r] = 1;
+                break;
+            }
+        }
+    }
+    // 4. parallel moves into homes
+    struct Mv { int dst, src; bool tr; };
+    std::vector<Mv> mv;
+    std::vector<uint8_t> isdst;
+    for (int X = 0; X < L0_; X++) {
+        if (!need[X]) continue;
+        const Val &v = loc_[X];
+        const int h = home_[X];
+        if (v.kind == K_CONST) {
+            // constant in this trace but symbolic in a merged successor
+            emit(U_LI, 0, h, 0, 0, v.c);
+            continue;
+        }
+        if (v.kind != K_REG) continue;
+        if (v.r == h && !v.tr) continue;
+        mv.push_back({h, v.r, v.tr});
+    }
+    isdst.assign(refcnt_.size() + 1, 0);
+    for (auto &m : mv) {
+        ensure_reg(m.dst);
+        if ((size_t)m.dst >= isdst.size()) isdst.resize(m.dst + 1, 0);
+        isdst[m.dst] = 1;
+    }
+    // preserve `keep` if a move overwrites its register
+    if (keep.kind == K_REG) {
+        bool clobbered = false;
+        for (auto &m : mv)
+            if (m.dst == keep.r && !(m.src == keep.r && m.tr && keep.tr)) clobbered = true;
+        if (clobbered) {
+            std::vector<uint8_t> ex = isdst;
+            for (auto &m : mv) {
+                if ((size_t)m.src >= ex.size()) ex.resize(m.src + 1, 0);
+                ex[m.src] = 1;
+            }
+            const int t = fresh_reg(&ex);
+            emit(U_MOV, fa(keep), t, keep.r, 0, 0);
+            keep.r = (uint16_t)t;
+            keep.tr = false;
+        }
+    }
+    while (!mv.empty()) {
+        bool progress = false;
+        for (size_t i = 0; i < mv.size(); i++) {
+            bool read = false;
+            for (size_t j = 0; j < mv.size() && !read; j++)
+                read = j != i && mv[j].src == mv[i].dst;
+            if (!read) {
+                emit(U_MOV, mv[i].tr ? UF_TA : 0, mv[i].dst, mv[i].src, 0, 0);
+                mv.erase(mv.begin() + i);
+                progress = true;
+                break;
+            }
+        }
+        if (progress) continue;
+        // only cycles left: park one destination's current content in a temp
+        const int d = mv[0].dst;
+        std::vector<uint8_t> ex(refcnt_.size() + 1, 0);
+        for (auto &m : mv) {
+            if ((size_t)std::max(m.dst, m.src) >= ex.size()) ex.resize(std::max(m.dst, m.src) + 1, 0);
+            ex[m.dst] = ex[m.src] = 1;
+        }
+        const int t = fresh_reg(&ex);
+        if (fail_) return keep;
+        emit(U_MOV, 0, t, d, 0, 0);
+        for (auto &m : mv)
+            if (m.src == d) m.src = t;
+    }
+    if (keep.kind == K_REG) ensure_reg(keep.r);
+    return keep;
+}
+
+void Compiler::exit_jump()
+{
+    std::vector<Ctl> succ{ctl_};
+    std::vector<std::vector<Val>> sl;
+    canonicalize(succ, sl, Val());
+    if (fail_) return;
+    const uint32_t id = get_or_create(succ[0], sl[0]);
+    emit(U_JUMP, 0, steps_ & 0xFFFF, steps_ >> 16, 0, 2 * (int64_t)id);
+}
+
+void Compiler::exit_end(uint8_t reason)
+{
+    const Val &o = loc_[OUTL()];
+    const uint8_t st = reason | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+    if (o.kind == K_REG) emit(U_END, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, 0, 0);
+    else emit(U_END, 0, st, 0, 0, o.kind == K_CONST ? o.c : 0);
+    emit_ext(steps_);
+}
+
+void Compiler::exit_branch(int n, uint8_t cond, uint16_t target)
+{
+    const uint32_t len = net_.len[n];
+    Ctl t = ctl_, f = ctl_;
+    t.ip[n] = target;
+    f.ip[n] = (uint16_t)((ctl_.ip[n] + 1 == len) ? 0 : ctl_.ip[n] + 1);
+    t.changed = f.changed = true;
+    t.pos = f.pos = (uint8_t)(n + 1);
+    steps_++;
+    std::vector<Ctl> succ{t, f};
+    std::vector<std::vector<Val>> sl;
+    const Val a = canonicalize(succ, sl, loc_[ACC(n)]);
+    if (fail_) return;
+    const uint32_t it = get_or_create(t, sl[0]);
+    const uint32_t iff = get_or_create(f, sl[1]);
+    const int64_t imm = (int64_t)(((uint64_t)(2 * iff) << 32) | (uint64_t)(2 * it));
+    emit(U_BR, (uint8_t)(fa(a) | (cond << UF_COND_SHIFT)), 0, a.r, 0, imm);
+    emit_ext(steps_);
+}
+
+void Compiler::exit_jro(int n, const Val &v)
+{
+    const uint32_t len = net_.len[n];
+    std::vector<Ctl> succ(len, ctl_);
+    for (uint32_t t = 0; t < len; t++) {
+        succ[t].ip[n] = (uint16_t)t;
+        succ[t].changed = true;
+        succ[t].pos = (uint8_t)(n + 1);
+    }
+    steps_++;
+    std::vector<std::vector<Val>> sl;
+    const Val a = canonicalize(succ, sl, v);
+    if (fail_) return;
+    const uint32_t off = (uint32_t)jtab_.size();
+    jtab_.resize(off + len);
+    for (uint32_t t = 0; t < len; t++) {
+        const uint32_t id = get_or_create(succ[t], sl[t]);
+        if (fail_) return;
+        jtab_[off + t] = 2 * id;
+    }
+    emit(U_JRO, fa(a), ctl_.ip[n], a.r, (uint16_t)(len - 1), off);
+    emit_ext(steps_);
+}
+
+void Compiler::round_end_marker()
+{
+    const Val &o = loc_[OUTL()];
+    const uint8_t st = MK_ST_BUDGET | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+    if (o.kind == K_REG) emit(U_ROUND_END, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, 0, 0);
+    else emit(U_ROUND_END, 0, st, 0, 0, o.kind == K_CONST ? o.c : 0);
+    emit_ext(steps_);
+}
+
+void Compiler::generalize()
+{
+    // constants that keep changing (a loop over constant data) prevent the
+    // state from ever repeating: turn every live constant into a register.
+    for (int X = 0; X < L0_; X++) {
+        if (loc_[X].kind != K_CONST) continue;
+        const int d = fresh_reg();
+        emit(U_LI, 0, d, 0, 0, loc_[X].c);
+        Val nv;
+        nv.kind = K_REG;
+        nv.r = (uint16_t)d;
+        set_loc(X, nv);
+        r32_[d] = is32(X);
+    }
+    for (int s = 0; s < S_; s++) {
+        for (uint32_t d = 0; d < (uint32_t)stk_[s].size(); d++) {
+            Val &v = stk_[s][d];
+            if (v.kind != K_CONST) continue;
+            const uint32_t slot = slot_of(s, d);
+            emit(U_STI, 0, 0, slot & 0xFFFF, slot >> 16, v.c);
+            digest_entry(dig_[s], d, v, false);
+            v = Val();
+            v.kind = K_MEM;
+            digest_entry(dig_[s], d, v, true);
+        }
+    }
+}
+
+int Compiler::attempt(int n)
+{
+    if ((ctl_.hung >> n) & 1u) return A_CONT;
+    const uint32_t len = net_.len[n];
+    uint16_t &ip = ctl_.ip[n];
+    const Insn &I = net_.code[net_.base[n] + ip];
+    auto retire = [&]() {
+        ip = (uint16_t)((ip + 1 == len) ? 0 : ip + 1);
+        steps_++;
+        ctl_.changed = true;
+    };
+    auto jump = [&](uint32_t t) {
+        ip = (uint16_t)t;
+        steps_++;
+        ctl_.changed = true;
+    };
+    const int A = ACC(n);
+    switch (I.op) {
+    case OP_NOP: retire(); return A_CONT;
+    case OP_SWP: std::swap(loc_[A], loc_[BAK(n)]); retire(); return A_CONT;
+    case OP_SAV: set_loc(BAK(n), loc_[A]); retire(); return A_CONT;
+    case OP_NEG: op_addsub(A, vconst(0), loc_[A], true); retire(); return A_CONT;
+    case OP_JMP: jump(I.arg); return A_CONT;
+    case OP_JEZ: case OP_JNZ: case OP_JGZ: case OP_JLZ: {
+        const Val &a = loc_[A];
+        if (a.kind == K_CONST) {
+            const int64_t v = a.c;
+            const bool take = (I.op == OP_JEZ && v == 0) || (I.op == OP_JNZ && v != 0) ||
+                              (I.op == OP_JGZ && v > 0) || (I.op == OP_JLZ && v < 0);
+            if (take) jump(I.arg);
+            else retire();
+            return A_CONT;
+        }
+        exit_branch(n, (uint8_t)(I.op - OP_JEZ), I.arg);
+        return A_EXIT;
+    }
+    case OP_STUCK: return A_CONT;
+    case OP_IN:
+        if (ctl_.in_avail) {
+            ctl_.in_avail = false;
+            if (I.dst) set_loc(A, loc_[INL()]);
+            set_loc(INL(), vdead());
+            retire();
+        }
+        return A_CONT;
+    case OP_POP: {
+        const int s = I.arg;
+        if (ctl_.depth[s] == 0) return A_CONT;
+        const uint32_t d = ctl_.depth[s] - 1;
+        Val e = stk_[s][d];
+        if (I.dst) {
+            if (e.kind == K_MEM) {
+                const int r = fresh_reg();
+                emit(U_LD, 0, r, 0, 0, slot_of(s, d));
+                Val nv;
+                nv.kind = K_REG;
+                nv.r = (uint16_t)r;
+                set_loc(A, nv);
+                r32_[r] = 1;
+            } else {
+                set_loc(A, e);
+            }
+        }
+        digest_entry(dig_[s], d, e, false);
+        decref(e);
+        stk_[s].pop_back();
+        ctl_.depth[s] = d;
+        retire();
+        return A_CONT;
+    }
+    default: break;
+    }
+    // ops with a source operand
+    const bool pn = (ctl_.pend >> n) & 1u;
+    Val v;
+    bool consumed = false;
+    if (pn) {
+        v = loc_[PENDV(n)];
+    } else if (I.src == SRC_IMM) {
+        v = vconst(I.imm);
+    } else if (I.src == SRC_ACC) {
+        v = loc_[A];
+    } else if (I.src == SRC_NIL) {
+        v = vconst(0);
+    } else {
+        const int slot = n * 4 + (I.src - SRC_R0);
+        if (!((ctl_.pfull >> slot) & 1ull)) return A_CONT; // receive blocks
+        v = loc_[PORT(slot)];
+        ctl_.pfull &= ~(1ull << slot);
+        consumed = true;
+    }
+    incref(v); // hold the operand for the duration of this attempt
+    if (consumed) set_loc(PORT(n * 4 + (I.src - SRC_R0)), vdead());
+    int rc = A_CONT;
+    switch (I.op) {
+    case OP_MOV:
+        if (I.dst) set_loc(A, v);
+        retire();
+        break;
+    case OP_ADD: op_addsub(A, loc_[A], v, false); retire(); break;
+    case OP_SUB: op_addsub(A, loc_[A], v, true); retire(); break;
+    case OP_JRO:
+        if (v.kind == K_CONST) {
+            int64_t t = wadd((int64_t)ip, v.c);
+            t = std::min<int64_t>(std::max<int64_t>(t, 0), (int64_t)len - 1);
+            jump((uint32_t)t);
+        } else {
+            exit_jro(n, v);
+            rc = A_EXIT;
+        }
+        break;
+    case OP_SEND: {
+        const int slot = I.arg;
+        if (!((ctl_.pfull >> slot) & 1ull)) {
+            set_loc(PORT(slot), trunc(v));
+            ctl_.pfull |= 1ull << slot;
+            ctl_.pend &= ~(1u << n);
+            set_loc(PENDV(n), vdead());
+            retire();
+        } else if (!pn) {
+            ctl_.pend |= 1u << n;
+            set_loc(PENDV(n), trunc(v));
+            ctl_.changed = true;
+        }
+        break;
+    }
+    case OP_OUT:
+        if (ctl_.out_cnt < 2) {
+            if (ctl_.out_cnt == 0) set_loc(OUTL(), trunc(v));
+            ctl_.out_cnt++;
+            ctl_.pend &= ~(1u << n);
+            set_loc(PENDV(n), vdead());
+            retire();
+            if (soo_) {
+                exit_end(MK_ST_OUTPUT_STOP);
+                rc = A_EXIT;
+            }
+        } else if (!pn) {
+            ctl_.pend |= 1u << n;
+            set_loc(PENDV(n), trunc(v));
+            ctl_.changed = true;
+        }
+        break;
+    case OP_PUSH: {
+        const int s = I.arg;
+        if (ctl_.depth[s] >= cap_) {
+            exit_end(MK_ST_STACK_OVERFLOW);
+            rc = A_EXIT;
+            break;
+        }
+        const Val e = trunc(v);
+        incref(e);
+        stk_[s].push_back(e);
+        digest_entry(dig_[s], ctl_.depth[s], e, true);
+        ctl_.depth[s]++;
+        retire();
+        break;
+    }
+    case OP_HANG:
+        ctl_.hung |= 1u << n;
+        ctl_.changed = true;
+        break;
+    case OP_RETRY:
+        if (consumed) ctl_.changed = true;
+        break;
+    default: break;
+    }
+    decref(v);
+    return rc;
+}
+
+void Compiler::compile_entry(uint32_t id)
+{
+    load_entry(id);
+    std::unordered_set<std::string> seen;
+    size_t last_size = 0;
+    uint32_t idle = 0;
+    for (;;) {
+        if (fail_) return;
+        if (ctl_.pos == N_) {
+            if (!ctl_.changed) {
+                exit_end(MK_ST_QUIESCENT);
+                break;
+            }
+            round_end_marker();
+            ctl_.pos = 0;
+            ctl_.changed = false;
+            if (++rounds_ > lim_.max_rounds) { failf("symbolic round budget exceeded"); return; }
+            prune(ctl_, loc_);
+            // prune() drops references without decref: rebuild the counts
+            std::fill(refcnt_.begin(), refcnt_.end(), 0);
+            for (int X = 0; X < L0_; X++) incref(loc_[X]);
+            for (int s = 0; s < S_; s++)
+                for (const Val &e : stk_[s]) incref(e);
+            const std::string k = key_of(ctl_, loc_, dig_);
+            if (memo_.count(k) || seen.count(k) || code_.size() > lim_.max_sb_uops) {
+                exit_jump();
+                break;
+            }
+            seen.insert(k);
+            idle = (code_.size() == last_size) ? idle + 1 : 0;
+            if (idle > lim_.idle_rounds) {
+                generalize();
+                idle = 0;
+            }
+            last_size = code_.size();
+            continue;
+        }
+        if (attempt(ctl_.pos) == A_EXIT) break;
+        ctl_.pos++;
+    }
+    if (fail_) return;
+    total_words_ += (uint32_t)code_.size() + 1;
+    if (total_words_ > lim_.max_uops) { failf("micro-op budget exceeded"); return; }
+    if (sb_code_.size() <= id) sb_code_.resize(id + 1);
+    sb_code_[id] = std::move(code_);
+    code_.clear();
+}
+
+bool Compiler::run(SchedProgram &out, std::string &why)
+{
+    if (N_ > 32) { why = "too many program nodes for the compiler"; return false; }
+    liveness();
+    // entry state: post-/reset, post-/run, input deposited (in register 0)
+    Ctl c;
+    c.ip.assign(N_, 0);
+    c.depth.assign(S_, 0);
+    ctl_ = c;
+    loc_.assign(L0_, vdead());
+    for (int n = 0; n < N_; n++) {
+        loc_[ACC(n)] = vconst(0);
+        loc_[BAK(n)] = vconst(0);
+    }
+    loc_[OUTL()] = vconst(0);
+    stk_.assign(S_, {});
+    dig_.assign(S_, StackDigest());
+    ensure_reg(0);
+    home_[INL()] = 0;
+    claimed_[0] = 1;
+    Val in;
+    in.kind = K_REG;
+    in.r = 0;
+    loc_[INL()] = in;
+    prune(ctl_, loc_);
+    get_or_create(ctl_, loc_);
+    while (!work_.empty() && !fail_) {
+        const uint32_t id = work_.front();
+        work_.pop_front();
+        compile_entry(id);
+    }
+    if (fail_) {
+        why = why_;
+        return false;
+    }
+    // assemble: per superblock a fast variant (GUARD + code without budget
+    // markers) and a checked variant (with markers)
+    out = SchedProgram();
+    out.entry.assign(2 * entries_.size(), 0);
+    for (size_t id = 0; id < entries_.size(); id++) {
+        const std::vector<UOp> &sc = sb_code_[id];
+        int64_t maxinc = -1;
+        for (size_t i = 0; i < sc.size(); i++) {
+            if (sc[i].op == U_ROUND_END) {
+                maxinc = std::max<int64_t>(maxinc, sc[i + 1].imm);
+                i++;
+            } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END) {
+                i++;
+            }
+        }
+        out.entry[2 * id] = (uint32_t)out.code.size();
+        if (maxinc >= 0) {
+            UOp g{};
+            g.op = U_GUARD;
+            g.d = (uint16_t)(maxinc & 0xFFFF);
+            g.a = (uint16_t)(maxinc >> 16);
+            g.imm = 2 * (int64_t)id + 1;
+            out.code.push_back(g);
+        }
+        for (size_t i = 0; i < sc.size(); i++) {
+            if (sc[i].op == U_ROUND_END) { i++; continue; }
+            out.code.push_back(sc[i]);
+        }
+        if (maxinc >= 0) {
+            out.entry[2 * id + 1] = (uint32_t)out.code.size();
+            out.code.insert(out.code.end(), sc.begin(), sc.end());
+        } else {
+            out.entry[2 * id + 1] = out.entry[2 * id];
+        }
+    }
+    out.jtab = jtab_;
+    out.nregs = std::max<uint32_t>(max_reg_, 1);
+    out.nslots = any_slot_ ? max_slot_ : 0;
+    out.in_reg = 0;
+    out.nsb = (uint32_t)entries_.size();
+    out.sym_rounds = rounds_;
+    return true;
+}
+
+} // namespace
+
+bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
+                      SchedProgram &out, std::string &why)
+{
+    Compiler c(net, stack_cap, stop_on_output, lim);
+    return c.run(out, why);
+}
+
+std::string sched_disasm(const SchedProgram &p)
+{
+    static const char *names[U_COUNT] = {"MOV", "LI", "ADD", "SUB", "ADDI", "RSUBI", "ST", "STI",
+                                         "LD", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END"};
+    std::string s;
+    char buf[200];
+    snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu\n", p.nsb, p.nregs, p.nslots,
+             p.code.size(), p.jtab.size());
+    s += buf;
+    std::vector<int> starts(p.code.size() + 1, -1);
+    for (size_t v = 0; v < p.entry.size(); v++)
+        if (starts[p.entry[v]] < 0) starts[p.entry[v]] = (int)v;
+    for (size_t i = 0; i < p.code.size(); i++) {
+        if (starts[i] >= 0) {
+            snprintf(buf, sizeof buf, "sb%d%s:\n", starts[i] / 2, (starts[i] & 1) ? " (checked)" : "");
+            s += buf;
+        }
+        const UOp &u = p.code[i];
+        const char *nm = u.op < U_COUNT ? names[u.op] : "?";
+        snprintf(buf, sizeof buf, "  %5zu %-9s fl=%02x d=%u a=%u b=%u imm=%lld\n", i, nm, u.fl, u.d, u.a, u.b,
+                 (long long)u.imm);
+        s += buf;
+        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END) {
+            i++;
+            snprintf(buf, sizeof buf, "        ext       steps+=%lld\n", (long long)p.code[i].imm);
+            s += buf;
+        }
+    }
+    return s;
+}
+
+} // namespace mk

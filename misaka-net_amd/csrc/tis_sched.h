@@ -1,0 +1,85 @@
+// tis_sched.h -- schedule compiler: lowers a network's canonical schedule
+// (SURVEY.md section 8.0 lane model) into "superblocks" of data micro-ops.
+//
+// Control state (instruction pointers, port full bits, pending sends, stack
+// depths, IN/OUT counters) only depends on data at JEZ/JNZ/JGZ/JLZ/JRO whose
+// operand is not a compile-time constant.  The compiler executes the
+// schedule symbolically on the host; every blocked attempt, every jump on a
+// constant, every register move, SWP, port hand-off and stack push/pop whose
+// value stays in a register costs nothing at run time.  What remains is a
+// short stream of int64 micro-ops per superblock, ending in a per-lane exit
+// (branch on data, multiway JRO, jump to a merged state, or END).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "tis_front.h"
+
+namespace mk {
+
+enum UOpCode : uint8_t {
+    U_MOV = 0,  // R[d] = A
+    U_LI,       // R[d] = imm
+    U_ADD,      // R[d] = A + B
+    U_SUB,      // R[d] = A - B
+    U_ADDI,     // R[d] = A + imm
+    U_RSUBI,    // R[d] = imm - A
+    U_ST,       // slot[imm] = int32(A)
+    U_STI,      // slot[a]   = int32(imm)
+    U_LD,       // R[d] = sext32(slot[imm])
+    U_JUMP,     // steps += d | a<<16; sb = imm                                  (1 word)
+    U_BR,       // steps += ext.imm; sb = cond(A) ? lo32(imm) : hi32(imm)         (2 words)
+    U_JRO,      // steps += ext.imm; sb = jtab[imm + clamp(d + A, 0, b)]          (2 words)
+    U_END,      // steps += ext.imm; out = OUTREG ? A : imm; status = d           (2 words)
+    U_GUARD,    // if steps + (d | a<<16) >= budget: sb = imm (checked variant)   (1 word)
+    U_ROUND_END,// if steps + ext.imm >= budget: END(status d, out A|imm)          (2 words)
+    U_COUNT
+};
+
+// A = R[a] (sign-extended low 32 bits when UF_TA), B likewise with UF_TB.
+enum : uint8_t { UF_TA = 1, UF_TB = 2, UF_OUTREG = 4 };
+// U_BR condition in fl bits 4..5: 0 = EZ, 1 = NZ, 2 = GZ, 3 = LZ
+constexpr int UF_COND_SHIFT = 4;
+
+struct UOp {
+    uint8_t op;
+    uint8_t fl;
+    uint16_t d;
+    uint16_t a;
+    uint16_t b;
+    int64_t imm;
+};
+static_assert(sizeof(UOp) == 16, "UOp must be 16 bytes");
+
+struct SchedLimits {
+    uint32_t max_superblocks = 16384;
+    uint32_t max_uops = 1u << 21;          // total words
+    uint32_t max_sb_uops = 1u << 17;       // words per superblock before generalising
+    uint32_t max_regs = 96;                // LDS registers per lane
+    uint32_t soft_regs = 24;               // above this, spill stack entries to HBM first
+    uint32_t idle_rounds = 64;             // rounds without emitted code before generalising
+    uint64_t max_rounds = 1ull << 22;      // symbolic rounds in total (compile-time bound)
+};
+
+struct SchedProgram {
+    std::vector<UOp> code;
+    std::vector<uint32_t> entry; // variant id -> first word; 2k = fast, 2k+1 = budget-checked
+    std::vector<uint32_t> jtab;  // JRO successor tables (variant ids)
+    uint32_t nregs = 0;          // 64-bit registers per lane (LDS)
+    uint32_t nslots = 0;         // stack memory slots per lane (HBM, lane-major)
+    uint32_t in_reg = 0;         // register holding the lane input at entry
+    uint32_t nsb = 0;            // superblocks
+    uint64_t sym_rounds = 0;     // rounds executed symbolically
+};
+
+// Compile for the given stack capacity / stop-on-output option (both change
+// the control flow).  Returns false with a reason when a limit is exceeded;
+// the caller then uses the direct bytecode interpreter.
+bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
+                      SchedProgram &out, std::string &why);
+
+std::string sched_disasm(const SchedProgram &p);
+
+} // namespace mk

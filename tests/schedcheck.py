@@ -1,0 +1,63 @@
+"""ctypes binding of lib/libmisaka_amd_check.so: the host model of the tier-2
+superblock executor (misaka-net_amd/csrc/sched_check.cpp), used to test the
+schedule compiler against the oracle without a GPU."""
+import ctypes as C
+import os
+
+import numpy as np
+
+import misaka_net_amd as mk
+from misaka_net_amd import _native as N
+
+LIB = os.path.join(os.path.dirname(mk._native.LIB_PATH), "libmisaka_amd_check.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        import __graft_entry__ as g
+
+        g.build_check()
+        h = C.CDLL(LIB)
+        h.mkc_load.restype = C.c_void_p
+        h.mkc_load.argtypes = [C.POINTER(N.mk_node_desc), C.c_int, C.c_char_p, C.c_size_t]
+        h.mkc_free.argtypes = [C.c_void_p]
+        h.mkc_emulate.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        _lib = h
+    return _lib
+
+
+class NotCompiled(Exception):
+    pass
+
+
+def emulate(nodes, xs, *, budget=None, stack_cap=None, stop_on_output=False, want_plan=False):
+    rows = [(n.name, n.kind, n.program) if hasattr(n, "name") else tuple(n) for n in nodes]
+    kinds = {"program": 0, "stack": 1, "master": 2}
+    arr = (N.mk_node_desc * len(rows))()
+    keep = []
+    for i, (nm, kd, pg) in enumerate(rows):
+        a, b = nm.encode(), (pg or "").encode()
+        keep += [a, b]
+        arr[i].name, arr[i].kind, arr[i].program = a, kinds[kd], b
+    err = C.create_string_buffer(4096)
+    h = lib().mkc_load(arr, len(rows), err, len(err))
+    assert h, err.value
+    try:
+        v = np.ascontiguousarray(np.asarray(xs, dtype=np.int64))
+        out = np.zeros(v.size, np.int32)
+        st = np.zeros(v.size, np.uint8)
+        sp = np.zeros(v.size, np.uint32)
+        why = C.create_string_buffer(512)
+        plan = C.create_string_buffer(1 << 22) if want_plan else None
+        rc = lib().mkc_emulate(h, budget or (1 << 20), 1024 if stack_cap is None else stack_cap,
+                               1 if stop_on_output else 0, v.ctypes.data, v.size, out.ctypes.data, st.ctypes.data,
+                               sp.ctypes.data, why, len(why), plan, len(plan) if plan is not None else 0)
+        if rc == 1:
+            raise NotCompiled(why.value.decode())
+        assert rc == 0, f"emulator error {rc}"
+        return (out, st, sp, plan.value.decode() if plan is not None else None)
+    finally:
+        lib().mkc_free(h)

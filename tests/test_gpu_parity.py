@@ -40,6 +40,10 @@ def test_readme_kat_on_gpu(gpu):
     assert (r.status == 0x11).all() and (r.steps == 12).all()
 
 
+TIERS = [pytest.param(False, id="compiled"), pytest.param(True, id="interp")]
+
+
+@pytest.mark.parametrize("interp", TIERS)
 @pytest.mark.parametrize(
     "name,nodes,n,gen",
     [
@@ -49,43 +53,57 @@ def test_readme_kat_on_gpu(gpu):
         ("c5_countdown", mk.networks.countdown_network(), 1 << 15, (N.MK_GEN_MASKED, 1023)),
     ],
 )
-def test_configs_bit_exact(gpu, name, nodes, n, gen):
+def test_configs_bit_exact(gpu, name, nodes, n, gen, interp):
     xs = po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1])
-    got = mk.Network(nodes).compute_batch(xs)
+    net = mk.Network(nodes)
+    if not interp:
+        assert net.plan().startswith("tier=compiled"), net.plan()
+    got = net.compute_batch(xs, interp=interp)
     assert_same(got, oracle(nodes, xs), name)
 
 
-def test_c4_deep_stacks_spill_to_hbm(gpu):
+@pytest.mark.parametrize("interp", TIERS)
+def test_c4_deep_stacks_spill_to_hbm(gpu, interp):
     nodes = mk.networks.pipeline_network(1024)
     xs = po.gen_inputs(SEED, 600)
-    got = mk.Network(nodes).compute_batch(xs)
+    got = mk.Network(nodes).compute_batch(xs, interp=interp)
     ref = oracle(nodes, xs)
     assert_same(got, ref, "c4 D=1024")
     assert (got.status == 0x11).all()
 
 
-def test_c5_zero_trip_and_maximum_trip(gpu):
+@pytest.mark.parametrize("interp", TIERS)
+def test_c5_zero_trip_and_maximum_trip(gpu, interp):
     nodes = mk.networks.countdown_network()
     xs = np.arange(0, 1024, dtype=np.int64)
-    assert_same(mk.Network(nodes).compute_batch(xs), oracle(nodes, xs), "c5 all trip counts")
+    assert_same(mk.Network(nodes).compute_batch(xs, interp=interp), oracle(nodes, xs), "c5 all trip counts")
 
 
+@pytest.mark.parametrize("interp", TIERS)
 @pytest.mark.parametrize("seed", range(0, 240, 1))
-def test_random_networks_bit_exact(gpu, seed):
+def test_random_networks_bit_exact(gpu, seed, interp):
     rows = random_network(seed)
     xs = po.gen_inputs(seed * 7919 + 1, 256)
     cap = [1, 3, 8, 16, 17, 40, 1024][seed % 7]
     kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=cap, stop_on_output=(seed % 5 == 4))
-    got = mk.Network(rows).compute_batch(xs, **kw)
+    got = mk.Network(rows).compute_batch(xs, interp=interp, **kw)
     assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
 
 
-def test_budget_and_stop_on_output(gpu):
+@pytest.mark.parametrize("interp", TIERS)
+def test_budget_and_stop_on_output(gpu, interp):
     nodes = [("a", "program", "JRO 0"), ("b", "program", "OUT 3\nJRO 0")]
-    got = mk.Network(nodes).compute_batch([0] * 70, budget=11)
+    got = mk.Network(nodes).compute_batch([0] * 70, budget=11, interp=interp)
     assert (got.steps == 12).all() and (got.status == (N.MK_ST_BUDGET | N.MK_ST_HAS_OUTPUT)).all()
-    got = mk.Network(nodes).compute_batch([0] * 70, stop_on_output=True)
+    got = mk.Network(nodes).compute_batch([0] * 70, stop_on_output=True, interp=interp)
     assert (got.steps == 2).all() and (got.status == (N.MK_ST_OUTPUT_STOP | N.MK_ST_HAS_OUTPUT)).all()
+
+
+@pytest.mark.parametrize("budget", [1, 11, 12, 13, 5000])
+def test_compiled_budget_boundaries(gpu, budget):
+    for nodes, kind in ((mk.networks.example_network(), 0), (mk.networks.countdown_network(), 1)):
+        xs = po.gen_inputs(SEED, 3000, kind=kind, mask=1023)
+        assert_same(mk.Network(nodes).compute_batch(xs, budget=budget), oracle(nodes, xs, budget=budget), str(budget))
 
 
 def test_empty_batch(gpu):
@@ -128,7 +146,7 @@ def test_device_generator_matches_oracle(gpu):
     assert np.array_equal(d.cpu().numpy(), po.gen_inputs(SEED, n, offset=12345).astype(np.int32))
 
 
-def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FULL, 0), offset=0):
+def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FULL, 0), offset=0, interp=False):
     import torch
 
     out = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -138,7 +156,7 @@ def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FU
     net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), steps_ptr=sp.data_ptr(),
                        stats_ptr=stats.data_ptr(), in_ptr=None if in_tensor is None else in_tensor.data_ptr(),
                        in_kind=in_kind, seed=SEED, gen_kind=gen[0], gen_mask=gen[1], offset=offset,
-                       stream=torch.cuda.current_stream().cuda_stream)
+                       stream=torch.cuda.current_stream().cuda_stream, interp=interp)
     torch.cuda.synchronize()
     return out.cpu().numpy(), st.cpu().numpy(), sp.cpu().numpy().view(np.uint32), stats.cpu().numpy()
 
@@ -161,7 +179,8 @@ def test_device_api_input_kinds_agree(gpu):
         assert r[3][1] == int(((ref[1] & 0x10) != 0).sum())
 
 
-def test_c2_full_size_properties(gpu):
+@pytest.mark.parametrize("interp", TIERS)
+def test_c2_full_size_properties(gpu, interp):
     # BASELINE config 2: 16,777,216 lanes; size-independent checks:
     # out == int32(x + 2) (README.md:39-44), 12 retired instrs, quiescent + output.
     import torch
@@ -170,7 +189,7 @@ def test_c2_full_size_properties(gpu):
     net = mk.Network(mk.networks.example_network())
     x = torch.empty(n, dtype=torch.int32, device="cuda")
     mk.generate_inputs_device(n, x.data_ptr(), seed=SEED, stream=torch.cuda.current_stream().cuda_stream)
-    out, st, sp, stats = _device_run(net, n, in_tensor=x)
+    out, st, sp, stats = _device_run(net, n, in_tensor=x, interp=interp)
     xe = x.cpu().numpy().astype(np.int64)
     assert np.array_equal(out, ((xe + 2 + 2**31) % 2**32 - 2**31).astype(np.int32))
     assert (st == 0x11).all() and (sp == 12).all()
@@ -181,14 +200,15 @@ def test_c2_full_size_properties(gpu):
     assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
 
 
-def test_c3_64m_shard_properties(gpu):
+@pytest.mark.parametrize("interp", TIERS)
+def test_c3_64m_shard_properties(gpu, interp):
     # BASELINE config 3 shards 67,108,864 lanes over 8 GPUs; one shard here
     # (lanes [7*8M, 8*8M)) with the global lane offset of rank 7.
     n = 1 << 23
     off = 7 * n
     nodes = mk.networks.sample_network()
     net = mk.Network(nodes)
-    out, st, sp, stats = _device_run(net, n, offset=off)
+    out, st, sp, stats = _device_run(net, n, offset=off, interp=interp)
     x = po.gen_inputs(SEED, n, offset=off)
     x32 = x.astype(np.int32).astype(np.int64)
     want = ((2 * x32 + 2**31) % 2**32 - 2**31).astype(np.int32)

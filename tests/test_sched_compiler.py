@@ -1,0 +1,70 @@
+"""Schedule compiler (tier 2, misaka-net_amd/csrc/tis_sched.cpp) against the
+oracle, executed by the host model of the superblock kernel
+(lib/libmisaka_amd_check.so) -- no GPU needed.  The GPU runs the same
+micro-op streams in tests/test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+import misaka_net_amd as mk
+from oracle import pyoracle as po
+import schedcheck as sc
+from tisgen import random_network
+
+SEED = 0x4D49534B41
+
+
+def same(nodes, xs, **kw):
+    o, s, p, _ = sc.emulate(nodes, xs, **kw)
+    ro, rs, rp = po.OracleNet(nodes).compute_batch(xs, **kw)
+    bad = np.nonzero((o != ro) | (s != rs) | (p != rp))[0]
+    assert not bad.size, (int(bad[0]), (o[bad[0]], s[bad[0]], p[bad[0]]), (ro[bad[0]], rs[bad[0]], rp[bad[0]]))
+
+
+@pytest.mark.parametrize("name", sorted(mk.networks.CONFIGS))
+def test_configs(name):
+    nodes = mk.networks.CONFIGS[name]()
+    kind = 1 if name.startswith("c5") else 0
+    xs = po.gen_inputs(SEED, 3000, kind=kind, mask=1023)
+    same(nodes, xs)
+
+
+def test_example_compiles_to_straight_line():
+    o, s, p, plan = sc.emulate(mk.networks.example_network(), [5], want_plan=True)
+    assert plan.splitlines()[0].startswith("superblocks=1 ")
+    fast = plan.split("(checked)")[0]
+    ops = [l.split()[1] for l in fast.splitlines()[2:] if l.startswith("  ") and not l.strip().startswith("ext")]
+    assert ops == ["GUARD", "ADDI", "ADDI", "END"], ops
+
+
+def test_deep_pipeline_d1024():
+    same(mk.networks.pipeline_network(1024), po.gen_inputs(SEED, 40))
+
+
+@pytest.mark.parametrize("budget", [1, 5, 11, 12, 13, 100])
+def test_budget_boundaries(budget):
+    same(mk.networks.example_network(), po.gen_inputs(SEED, 64), budget=budget)
+    same(mk.networks.countdown_network(), po.gen_inputs(SEED, 64, kind=1, mask=1023), budget=budget * 37)
+
+
+def test_stop_on_output_and_overflow():
+    same(mk.networks.sample_network(), po.gen_inputs(SEED, 200), stop_on_output=True)
+    same(mk.networks.pipeline_network(64), po.gen_inputs(SEED, 20), stack_cap=63)
+
+
+def test_constant_spin_loops_generalise():
+    nodes = [("a", "program", "L: ADD 1\nJMP L"), ("b", "program", "IN ACC\nJRO 0")]
+    same(nodes, [1, 2, 3], budget=5000)
+
+
+def test_random_networks():
+    declined = 0
+    for seed in range(0, 600):
+        rows = random_network(seed)
+        xs = po.gen_inputs(seed * 7919 + 1, 48)
+        kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=[1, 3, 8, 16, 17, 40, 1024][seed % 7],
+                  stop_on_output=(seed % 5 == 4))
+        try:
+            same(rows, xs, **kw)
+        except sc.NotCompiled:
+            declined += 1
+    assert declined < 30
