@@ -133,8 +133,9 @@ def main():
     # Inputs resident in HBM before the timed region (global lane indices
     # [rank*lanes, (rank+1)*lanes)).
     x = torch.empty(lanes, dtype=torch.int32, device="cuda")
+    lo, _ = mk.dist.shard(rank, lanes)
     mk.generate_inputs_device(lanes, x.data_ptr(), seed=SEED, gen_kind=gen_kind, gen_mask=mask,
-                              offset=rank * lanes, device=dev, stream=sh)
+                              offset=lo, device=dev, stream=sh)
     out = torch.empty(lanes, dtype=torch.int32, device="cuda")
     st = torch.empty(lanes, dtype=torch.uint8, device="cuda")
     stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
@@ -164,10 +165,9 @@ def main():
 
     # per-rank -> whole job (max time over ranks, summed work)
     t = torch.tensor([wall, kernel_s], dtype=torch.float64, device="cuda")
-    tot = stats.clone()
+    tot = mk.dist.reduce_counters(stats.clone(), dist)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     wall_max, kern_max = t.tolist()
     tot = tot.cpu().numpy()
     retired, with_out, finished = int(tot[0]), int(tot[1]), int(tot[2])
@@ -176,13 +176,10 @@ def main():
     gather_ms = None
     if args.gather and dist:
         torch.cuda.synchronize()
-        g_out = torch.empty(lanes * world if rank == 0 else 1, dtype=torch.int32, device="cuda")
         dist.barrier()
         tg = time.perf_counter()
-        if rank == 0:
-            dist.gather(out, gather_list=list(g_out.view(world, lanes).unbind(0)), dst=0)
-        else:
-            dist.gather(out, dst=0)
+        mk.dist.gather_outputs(out, dist)
+        mk.dist.gather_outputs(st, dist)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 

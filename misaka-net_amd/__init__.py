@@ -15,7 +15,7 @@ from .network import (
     tokenize,
     valu_probe_device,
 )
-from . import networks
+from . import dist, networks
 
 __all__ = [
     "BatchResult",
@@ -26,5 +26,6 @@ __all__ = [
     "tokenize",
     "valu_probe_device",
     "networks",
+    "dist",
     "_native",
 ]

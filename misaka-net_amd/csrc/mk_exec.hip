@@ -407,7 +407,13 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const UOp *__restrict__
     uint64_t idx = gid;
     bool active = idx < p.n;
     uint32_t sb = 0, steps = 0;
-    if (active) reg(p.in_reg) = sched_input(p, idx);
+    // The next input of this lane is loaded one input ahead, so a refill
+    // never waits on HBM latency.
+    int32_t next_in = 0;
+    if (active) {
+        reg(p.in_reg) = sched_input(p, idx);
+        if (idx + p.lanes < p.n) next_in = sched_input(p, idx + p.lanes);
+    }
 
     for (;;) {
         const unsigned long long act = __ballot(active);
@@ -511,7 +517,10 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const UOp *__restrict__
             active = idx < p.n;
             sb = 0;
             steps = 0;
-            if (active) reg(p.in_reg) = sched_input(p, idx);
+            if (active) {
+                reg(p.in_reg) = next_in;
+                if (idx + p.lanes < p.n) next_in = sched_input(p, idx + p.lanes);
+            }
         }
     }
 

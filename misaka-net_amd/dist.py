@@ -1,0 +1,40 @@
+"""Multi-GPU plumbing for the batched /compute path (SURVEY.md section 8 row e).
+
+The lane batch shards with no exchange: rank r of W evaluates global lane
+indices [r*n, (r+1)*n).  RCCL (torch.distributed "nccl") is used only for the
+counter reduction and the optional ordered output gather to rank 0.
+"""
+from __future__ import annotations
+
+
+def shard(rank: int, lanes_per_rank: int) -> tuple[int, int]:
+    """[lo, hi) global lane indices of `rank` (weak scaling: fixed per-rank size)."""
+    return rank * lanes_per_rank, (rank + 1) * lanes_per_rank
+
+
+def split(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous split of a fixed global batch (strong scaling)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def reduce_counters(stats, dist):
+    """Sum the per-rank executor counters (uint64[MK_STATS_LEN] as int64)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return stats
+
+
+def gather_outputs(out, dist, dst: int = 0):
+    """Ordered gather of equal-size per-rank output shards to rank `dst`:
+    returns the concatenation in rank (= global lane) order on dst, None elsewhere."""
+    import torch
+
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return out
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if rank == dst:
+        buf = torch.empty(world * out.numel(), dtype=out.dtype, device=out.device)
+        dist.gather(out, gather_list=list(buf.view(world, -1).unbind(0)), dst=dst)
+        return buf
+    dist.gather(out, dst=dst)
+    return None
