@@ -15,7 +15,7 @@ from .network import (
     tokenize,
     valu_probe_device,
 )
-from . import dist, networks
+from . import dist, master, networks
 
 __all__ = [
     "BatchResult",
@@ -27,5 +27,6 @@ __all__ = [
     "valu_probe_device",
     "networks",
     "dist",
+    "master",
     "_native",
 ]

@@ -369,9 +369,18 @@ struct SParams {
     uint32_t in_reg;
 };
 
+// `i` must be wave-uniform.  readfirstlane pins the index and every fetched
+// dword to SGPRs: the load becomes one s_load_dwordx4 and the opcode switch a
+// scalar branch (without it the compiler loses uniformity through the
+// dispatch loop and emits vector loads plus an exec-masked case chain).
 __device__ __forceinline__ UOp fetch_uop(const UOp *__restrict__ code, uint32_t i)
 {
-    const uint4 w = reinterpret_cast<const uint4 *>(code)[i];
+    i = __builtin_amdgcn_readfirstlane(i);
+    uint4 w = reinterpret_cast<const uint4 *>(code)[i];
+    w.x = __builtin_amdgcn_readfirstlane(w.x);
+    w.y = __builtin_amdgcn_readfirstlane(w.y);
+    w.z = __builtin_amdgcn_readfirstlane(w.z);
+    w.w = __builtin_amdgcn_readfirstlane(w.w);
     UOp u;
     u.op = (uint8_t)(w.x & 0xffu);
     u.fl = (uint8_t)((w.x >> 8) & 0xffu);
@@ -421,7 +430,7 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const UOp *__restrict__
         const int lead = __builtin_ctzll(act);
         const uint32_t u = __builtin_amdgcn_readlane(sb, lead);
         if (!(active && sb == u)) continue;
-        uint32_t pc = entry[u]; // wave-uniform
+        uint32_t pc = __builtin_amdgcn_readfirstlane(entry[__builtin_amdgcn_readfirstlane(u)]); // wave-uniform
         bool done = false;
         uint32_t st = 0;
         int32_t outv = 0;

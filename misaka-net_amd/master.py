@@ -1,0 +1,278 @@
+"""The master node's HTTP surface (internal/nodes/master.go:90-227) over the
+batched GPU executor -- SURVEY.md section 8 row f1.
+
+Routes, methods, status codes and error texts follow master.go:
+  POST /run      -> "Success"                      (master.go:90-106)
+  POST /pause    -> "Success"                      (master.go:108-124)
+  POST /reset    -> "Success"                      (master.go:126-143)
+  POST /load     program, targetURI -> "Success"   (master.go:145-195)
+  POST /compute  value -> {"value": N}\\n           (master.go:197-224)
+  any other method -> 405 "method GET not allowed"
+Added: POST /compute_batch with repeated ``value`` fields (or a JSON body
+``{"values": [...]}``) -> {"values": [...], "status": [...]}, evaluated as
+one GPU batch.
+
+Deliberate differences (DESIGN.md / INTEGRATION.md):
+  * /load reaches the program node (the reference dials targetURI:8000 while
+    program nodes serve :8001, master.go:178, so its /load never completes);
+    a rejected program answers 400 "error loading program on node X: <Go
+    error text>" and leaves the previous program in place (program.go:180-192).
+  * every /compute runs on a fresh post-/reset copy of the network (the lane
+    model); the reference keeps node state between calls (row f2, next).
+  * a /compute whose network produces no output answers 504 "network
+    produced no output" instead of hanging forever.
+"""
+from __future__ import annotations
+
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Mapping, Optional
+from urllib.parse import unquote_to_bytes
+
+import numpy as np
+
+from . import _native as N
+from .network import Network, NodeSpec, TisParseError, tokenize
+
+
+class FormError(ValueError):
+    pass
+
+
+def _unescape(s: str) -> str:
+    # url.QueryUnescape: '+' -> ' ', %XX must be two hex digits
+    i = 0
+    while True:
+        i = s.find("%", i)
+        if i < 0:
+            break
+        h = s[i + 1: i + 3]
+        if len(h) != 2 or any(c not in "0123456789abcdefABCDEF" for c in h):
+            raise FormError("invalid URL escape")
+        i += 3
+    return unquote_to_bytes(s.replace("+", " ")).decode("utf-8", "surrogateescape")
+
+
+def parse_query(q: str) -> dict:
+    """Go 1.14 url.ParseQuery: pairs split on '&' and ';', first error wins."""
+    out: dict = {}
+    for part in q.replace(";", "&").split("&"):
+        if not part:
+            continue
+        k, _, v = part.partition("=")
+        out.setdefault(_unescape(k), []).append(_unescape(v))
+    return out
+
+
+def go_atoi(s: str) -> int:
+    """strconv.Atoi on a 64-bit platform."""
+    if not s:
+        raise ValueError("invalid syntax")
+    body = s[1:] if s[0] in "+-" else s
+    if not body or any(c not in "0123456789" for c in body):
+        raise ValueError("invalid syntax")
+    v = int(s)
+    if not -(2**63) <= v < 2**63:
+        raise ValueError("value out of range")
+    return v
+
+
+class Response:
+    def __init__(self, code: int, body: str, ctype: str = "text/plain; charset=utf-8"):
+        self.code, self.body, self.ctype = code, body, ctype
+
+
+def http_error(msg: str, code: int) -> Response:
+    return Response(code, msg + "\n")  # http.Error appends a newline
+
+
+class MasterNode:
+    """In-process master: the request handlers of master.go over a Network.
+
+    ``node_info``: NODE_INFO (name -> {"type": "program"|"stack"});
+    ``programs``: the PROGRAM text each program node booted with;
+    ``name``: the master's own service name (MASTER_URI of the nodes).
+    """
+
+    def __init__(self, node_info: Mapping[str, Mapping], programs: Optional[Mapping[str, str]] = None,
+                 name: str = "last_order", devices=None, budget=None, stack_cap=None):
+        self.node_info = {k: dict(v) for k, v in node_info.items()}
+        self.name = name
+        self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
+        self.devices, self.budget, self.stack_cap = devices, budget, stack_cap
+        self.is_running = False
+        self._lock = threading.Lock()
+        # cmd/app.go:21-24: a PROGRAM that fails to load is logged and the node
+        # keeps its default program ([["NOP"]], program.go:64)
+        for k, text in (programs or {}).items():
+            if k in self.programs:
+                try:
+                    tokenize(text)
+                    self.programs[k] = text
+                except TisParseError:
+                    pass
+        self._net = None
+
+    # -- network handle ------------------------------------------------------
+    def _specs(self):
+        specs = []
+        for k, v in self.node_info.items():
+            t = v.get("type")
+            if t not in ("program", "stack"):
+                raise ValueError("invalid node type")  # master.go:437
+            specs.append(NodeSpec(k, t, self.programs.get(k, "")))
+        specs.append(NodeSpec(self.name, "master"))
+        return specs
+
+    def network(self) -> Network:
+        if self._net is None:
+            self._net = Network(self._specs())
+        return self._net
+
+    # -- handlers -------------------------------------------------------------
+    def handle(self, method: str, path: str, query: str = "", body: bytes = b"", ctype: str = "") -> Response:
+        routes = {"/run": self._run, "/pause": self._pause, "/reset": self._reset, "/load": self._load,
+                  "/compute": self._compute, "/compute_batch": self._compute_batch}
+        fn = routes.get(path)
+        if fn is None:
+            return Response(404, "404 page not found\n")
+        if method != "POST":
+            return http_error("method GET not allowed", 405)
+        return fn(query, body, ctype)
+
+    def _form(self, query, body, ctype) -> dict:
+        form = parse_query(query)
+        if ctype.split(";")[0].strip().lower() == "application/x-www-form-urlencoded":
+            for k, v in parse_query(body.decode("latin-1")).items():
+                form.setdefault(k, [])
+                form[k] = v + form[k]  # body values take precedence (r.Form order)
+        return form
+
+    def _check_types(self):
+        for v in self.node_info.values():
+            if v.get("type") not in ("program", "stack"):
+                return "invalid node type"
+        return None
+
+    def _run(self, *_):
+        with self._lock:
+            self.is_running = True  # master.go:93 sets it before broadcasting
+            e = self._check_types()
+            if e:
+                return http_error(f"error running network: {e}", 400)
+            return Response(200, "Success")
+
+    def _pause(self, *_):
+        with self._lock:
+            e = self._check_types()
+            if e:
+                return http_error(f"error pausing network: {e}", 400)
+            self.is_running = False
+            return Response(200, "Success")
+
+    def _reset(self, *_):
+        with self._lock:
+            e = self._check_types()
+            if e:
+                return http_error(f"error resetting network: {e}", 400)
+            self.is_running = False
+            return Response(200, "Success")
+
+    def _load(self, query, body, ctype):
+        try:
+            form = self._form(query, body, ctype)
+        except FormError:
+            return http_error("cannot parse form", 400)
+        program = (form.get("program") or [""])[0]
+        target = (form.get("targetURI") or [""])[0]
+        with self._lock:
+            if target not in self.node_info:
+                err = f"node {target} not valid on this network"
+                return http_error(f"error loading program on node {target}: {err}", 400)
+            e = self._check_types()
+            if e:
+                return http_error(f"error resetting network: {e}", 400)
+            self.is_running = False  # /load resets the network first (master.go:166-175)
+            if self.node_info[target].get("type") != "program":
+                return http_error(f"error loading program on node {target}: not a program node", 400)
+            try:
+                tokenize(program)  # ProgramNode.LoadProgram's parse (program.go:178-193)
+            except TisParseError as ex:
+                return http_error(f"error loading program on node {target}: {ex}", 400)
+            self.programs[target] = program
+            if self._net is not None:
+                self._net.close()
+                self._net = None
+            return Response(200, "Success")
+
+    def _values(self, form, key="value"):
+        return form.get(key) or [""]
+
+    def _compute(self, query, body, ctype):
+        if not self.is_running:
+            return http_error("network is not running", 400)
+        try:
+            form = self._form(query, body, ctype)
+        except FormError:
+            return http_error("cannot parse form", 400)
+        try:
+            v = go_atoi(self._values(form)[0])
+        except ValueError:
+            return http_error("cannot parse value", 400)
+        with self._lock:
+            r = self.network().compute_batch([v], budget=self.budget, stack_cap=self.stack_cap,
+                                             devices=self.devices, steps=False)
+        if not (int(r.status[0]) & N.MK_ST_HAS_OUTPUT):
+            return http_error("network produced no output", 504)
+        return Response(200, json.dumps({"value": int(r.out[0])}) + "\n", "application/json")
+
+    def _compute_batch(self, query, body, ctype):
+        if not self.is_running:
+            return http_error("network is not running", 400)
+        try:
+            if ctype.split(";")[0].strip().lower() == "application/json":
+                vals = [int(v) for v in json.loads(body.decode() or "{}").get("values", [])]
+                for v in vals:
+                    if not -(2**63) <= v < 2**63:
+                        raise ValueError
+            else:
+                vals = [go_atoi(s) for s in self._form(query, body, ctype).get("value", [])]
+        except FormError:
+            return http_error("cannot parse form", 400)
+        except (ValueError, TypeError, AttributeError):
+            return http_error("cannot parse value", 400)
+        with self._lock:
+            r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
+                                             stack_cap=self.stack_cap, devices=self.devices, steps=False)
+        has = (r.status & N.MK_ST_HAS_OUTPUT) != 0
+        out = {"values": [int(x) if h else None for x, h in zip(r.out, has)], "status": r.status.tolist()}
+        return Response(200, json.dumps(out) + "\n", "application/json")
+
+
+def make_server(master: MasterNode, host: str = "127.0.0.1", port: int = 8000) -> ThreadingHTTPServer:
+    """HTTP/1.1 server on :8000 (clientPort, master.go:18) around `master`."""
+
+    class Handler(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def _do(self):
+            path, _, query = self.path.partition("?")
+            n = int(self.headers.get("Content-Length") or 0)
+            body = self.rfile.read(n) if n else b""
+            r = master.handle(self.command, path, query, body, self.headers.get("Content-Type", ""))
+            data = r.body.encode()
+            self.send_response(r.code)
+            self.send_header("Content-Type", r.ctype)
+            if r.code >= 400:
+                self.send_header("X-Content-Type-Options", "nosniff")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+        do_GET = do_POST = do_PUT = do_DELETE = do_PATCH = _do
+
+        def log_message(self, *a):
+            pass
+
+    return ThreadingHTTPServer((host, port), Handler)
