@@ -58,7 +58,7 @@ struct KParams {
     int32_t *out;
     uint8_t *status;
     uint32_t *steps;
-    unsigned long long *stats;
+    unsigned long long *partials; // [waves][8] per-wave counters, or null
     uint32_t stack_cap;
     uint32_t flags;
     uint32_t ring;       // LDS ring entries per stack (power of two), 0 = no stacks
@@ -107,6 +107,39 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+
+__device__ __forceinline__ void write_partials(unsigned long long *partials, uint64_t gid,
+                                               const unsigned long long (&c)[7])
+{
+    unsigned long long v[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) v[k] = wave_sum(c[k]);
+    if ((gid & 63) == 0) {
+        unsigned long long *q = partials + (gid >> 6) * 8;
+#pragma unroll
+        for (int k = 0; k < 7; k++) q[k] = v[k];
+        q[7] = 0;
+    }
+}
+
+// One block folds the per-wave partials into the caller's counters
+// (8 atomics per launch instead of 7 per wave on the same lines).
+__global__ void __launch_bounds__(256) stats_reduce(const unsigned long long *__restrict__ partials,
+                                                    uint32_t nwaves, unsigned long long *stats)
+{
+    __shared__ unsigned long long acc[256];
+    const uint32_t t = threadIdx.x, k = t & 7;
+    unsigned long long s = 0;
+    for (uint32_t w = t >> 3; w < nwaves; w += 32) s += partials[(size_t)w * 8 + k];
+    acc[t] = s;
+    __syncthreads();
+    if (t < 8) {
+        unsigned long long tot = 0;
+        for (int g = 0; g < 32; g++) tot += acc[g * 8 + t];
+        if (tot) atomicAdd(&stats[t], tot);
+    }
+}
+
 
 // Fetch one 16-byte instruction with a wave-uniform address as four dwords,
 // so it is a single scalar load (SMEM has no byte loads) and every decoded
@@ -324,19 +357,9 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
         }
     }
 
-    if (p.stats) {
-        const unsigned long long v0 = wave_sum(s_steps), v1 = wave_sum(s_out), v2 = wave_sum(s_done),
-                                 v3 = wave_sum(s_q), v4 = wave_sum(s_b), v5 = wave_sum(s_ov),
-                                 v6 = wave_sum(s_os);
-        if ((tid & 63) == 0 && v2) {
-            atomicAdd(&p.stats[0], v0);
-            atomicAdd(&p.stats[1], v1);
-            atomicAdd(&p.stats[2], v2);
-            if (v3) atomicAdd(&p.stats[3], v3);
-            if (v4) atomicAdd(&p.stats[4], v4);
-            if (v5) atomicAdd(&p.stats[5], v5);
-            if (v6) atomicAdd(&p.stats[6], v6);
-        }
+    if (p.partials) {
+        const unsigned long long c[7] = {s_steps, s_out, s_done, s_q, s_b, s_ov, s_os};
+        write_partials(p.partials, gid, c);
     }
 }
 
@@ -363,32 +386,33 @@ struct SParams {
     int32_t *out;
     uint8_t *status;
     uint32_t *steps;
-    unsigned long long *stats;
-    int32_t *slots;   // [nslots][lanes]
-    uint64_t lanes;   // resident lanes
-    uint32_t in_reg;
+    unsigned long long *partials; // [waves][8] per-wave counters, or null
+    int32_t *slots;      // [nslots][vlanes] stack slots in HBM
+    uint64_t lanes;      // resident threads
+    uint64_t vlanes;     // lanes * K (one input per slot)
+    uint32_t in_off;     // LDS byte offset of the input register within a slot
+    uint32_t slot_bytes; // LDS bytes of one slot's register file (nregs * block * 8)
 };
 
 // `i` must be wave-uniform.  readfirstlane pins the index and every fetched
-// dword to SGPRs: the load becomes one s_load_dwordx4 and the opcode switch a
-// scalar branch (without it the compiler loses uniformity through the
-// dispatch loop and emits vector loads plus an exec-masked case chain).
-__device__ __forceinline__ UOp fetch_uop(const UOp *__restrict__ code, uint32_t i)
+// dword to SGPRs: the fetch is scalar loads and the opcode switch a scalar
+// branch (without it the compiler loses uniformity through the dispatch loop
+// and emits vector loads plus an exec-masked case chain).
+__device__ __forceinline__ DOp fetch_dop(const DOp *__restrict__ code, uint32_t i)
 {
     i = __builtin_amdgcn_readfirstlane(i);
-    uint4 w = reinterpret_cast<const uint4 *>(code)[i];
-    w.x = __builtin_amdgcn_readfirstlane(w.x);
-    w.y = __builtin_amdgcn_readfirstlane(w.y);
-    w.z = __builtin_amdgcn_readfirstlane(w.z);
-    w.w = __builtin_amdgcn_readfirstlane(w.w);
-    UOp u;
-    u.op = (uint8_t)(w.x & 0xffu);
-    u.fl = (uint8_t)((w.x >> 8) & 0xffu);
-    u.d = (uint16_t)(w.x >> 16);
-    u.a = (uint16_t)(w.y & 0xffffu);
-    u.b = (uint16_t)(w.y >> 16);
-    u.imm = (int64_t)(((uint64_t)w.w << 32) | (uint64_t)w.z);
-    return u;
+    const uint4 *q = reinterpret_cast<const uint4 *>(code) + 2 * (size_t)i;
+    const uint4 w0 = q[0], w1 = q[1];
+    DOp o;
+    o.op = __builtin_amdgcn_readfirstlane(w0.x);
+    o.fl = __builtin_amdgcn_readfirstlane(w0.y);
+    o.d = __builtin_amdgcn_readfirstlane(w0.z);
+    o.a = __builtin_amdgcn_readfirstlane(w0.w);
+    o.b = __builtin_amdgcn_readfirstlane(w1.x);
+    o.inc = __builtin_amdgcn_readfirstlane(w1.y);
+    o.imm = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane(w1.w) << 32) |
+                      (uint64_t)__builtin_amdgcn_readfirstlane(w1.z));
+    return o;
 }
 
 __device__ __forceinline__ int32_t sched_input(const SParams &p, uint64_t i)
@@ -398,155 +422,220 @@ __device__ __forceinline__ int32_t sched_input(const SParams &p, uint64_t i)
     return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
 }
 
-__global__ void __launch_bounds__(kBlock) tis_sched_exec(const UOp *__restrict__ code,
+// Runs superblock micro-ops from `pc` for the slots flagged in `mine` until
+// the group exits.  FULL: every thread taking part has all K slots in the
+// group, so no per-slot masking is emitted.  CHECKED: the budget-checked
+// variant, where ROUND_END can end single slots.
+template <int K, bool FULL, bool CHECKED>
+__device__ __forceinline__ void run_superblock(const DOp *__restrict__ code, const uint32_t *__restrict__ jtab,
+                                               const SParams &p, char *lane_base, uint32_t kstride,
+                                               uint64_t vlane0, uint32_t pc, bool (&mine)[K], uint32_t (&sb)[K],
+                                               uint32_t (&steps)[K], bool (&done)[K], uint32_t (&st)[K],
+                                               int32_t (&outv)[K])
+{
+    auto reg = [&](int k, uint32_t off) -> int64_t & {
+        return *reinterpret_cast<int64_t *>(lane_base + (uint32_t)k * kstride + off);
+    };
+    auto opnd = [&](int k, uint32_t off, uint32_t t) -> int64_t {
+        const int64_t v = reg(k, off);
+        return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v;
+    };
+    // HBM stack slots are [slot][virtual lane], virtual lane = k * lanes + gid
+    auto slot = [&](int k, uint64_t s) -> int32_t & {
+        return p.slots[s * p.vlanes + vlane0 + (uint64_t)k * p.lanes];
+    };
+#define MK_SLOTS for (int k = 0; k < K; ++k) if (FULL || mine[k])
+    for (;;) {
+        const DOp I = fetch_dop(code, pc);
+        const uint32_t ta = I.fl & UF_TA, tb = I.fl & UF_TB;
+        bool leave = false;
+        // ordered by frequency in compiled schedules (the scalar unit is the
+        // bottleneck: a hot op should cost one compare)
+        if (I.op == U_ADDI) {
+            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) + (uint64_t)I.imm);
+        } else if (I.op == U_MOV) {
+            MK_SLOTS reg(k, I.d) = opnd(k, I.a, ta);
+        } else if (I.op == U_BR) {
+            const uint32_t cond = (I.fl >> UF_COND_SHIFT) & 3u;
+            MK_SLOTS {
+                const int64_t v = opnd(k, I.a, ta);
+                const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
+                steps[k] += I.inc;
+                sb[k] = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
+            }
+            leave = true;
+        } else if (I.op == U_END) {
+            MK_SLOTS {
+                steps[k] += I.inc;
+                outv[k] = (I.fl & UF_OUTREG) ? (int32_t)opnd(k, I.a, ta) : (int32_t)I.imm;
+                st[k] = I.d;
+                done[k] = true;
+            }
+            leave = true;
+        } else if (I.op == U_JUMP) {
+            MK_SLOTS {
+                steps[k] += I.inc;
+                sb[k] = (uint32_t)I.imm;
+            }
+            leave = true;
+        } else if (!CHECKED && I.op == U_GUARD) {
+            // any slot that could reach the budget inside: the whole group
+            // takes the checked variant (exact for every slot)
+            bool need = false;
+            MK_SLOTS need = need || (uint64_t)steps[k] + I.inc >= p.budget;
+            if (__ballot(need)) {
+                MK_SLOTS sb[k] = (uint32_t)I.imm;
+                leave = true;
+            }
+        } else if (I.op == U_ADD) {
+            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) + (uint64_t)opnd(k, I.b, tb));
+        } else if (I.op == U_SUB) {
+            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) - (uint64_t)opnd(k, I.b, tb));
+        } else if (I.op == U_RSUBI) {
+            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)I.imm - (uint64_t)opnd(k, I.a, ta));
+        } else if (I.op == U_LD) {
+            MK_SLOTS reg(k, I.d) = slot(k, (uint64_t)I.imm);
+        } else if (I.op == U_ST) {
+            MK_SLOTS slot(k, (uint64_t)I.imm) = (int32_t)opnd(k, I.a, ta);
+        } else if (I.op == U_LI) {
+            MK_SLOTS reg(k, I.d) = I.imm;
+        } else if (I.op == U_STI) {
+            MK_SLOTS slot(k, I.d) = (int32_t)I.imm;
+        } else if (I.op == U_JRO) {
+            MK_SLOTS {
+                // IntClamp(ptr+v, 0, len-1) with an int64 wrapping add (program.go:354,362)
+                int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)opnd(k, I.a, ta));
+                t = t > (int64_t)I.b ? (int64_t)I.b : t;
+                t = t < 0 ? 0 : t;
+                steps[k] += I.inc;
+                sb[k] = jtab[(uint64_t)I.imm + (uint64_t)t];
+            }
+            leave = true;
+        } else if (CHECKED && I.op == U_ROUND_END) {
+            bool left = false;
+            MK_SLOTS {
+                if ((uint64_t)steps[k] + I.inc >= p.budget) {
+                    steps[k] += I.inc;
+                    outv[k] = (I.fl & UF_OUTREG) ? (int32_t)opnd(k, I.a, ta) : (int32_t)I.imm;
+                    st[k] = I.d;
+                    done[k] = true;
+                    mine[k] = false;
+                }
+                left = left || mine[k];
+            }
+            if (!__ballot(left)) leave = true; // every slot of the group stopped here
+        } else {
+            MK_SLOTS { // corrupt stream: end the slots
+                st[k] = 0;
+                done[k] = true;
+            }
+            leave = true;
+        }
+        if (leave) break;
+        ++pc;
+    }
+#undef MK_SLOTS
+}
+
+// Tier-2 kernel: each thread carries K independent inputs ("slots"); one
+// scalar fetch + dispatch of a micro-op serves all K x 64 of them.
+template <int K>
+__global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__ code,
                                                          const uint32_t *__restrict__ entry,
                                                          const uint32_t *__restrict__ jtab, SParams p)
 {
-    extern __shared__ int64_t R[]; // [nregs][blockDim.x]
-    const uint32_t B = blockDim.x;
+    extern __shared__ int64_t R[]; // [K][nregs][blockDim.x] 64-bit registers
     const uint32_t tid = threadIdx.x;
-    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
-    auto reg = [&](uint32_t r) -> int64_t & { return R[r * B + tid]; };
-    auto opnd = [&](uint32_t r, bool t) -> int64_t {
-        const int64_t v = reg(r);
-        return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + tid;
+    char *const lane_base = reinterpret_cast<char *>(R) + tid * 8;
+    const uint32_t kstride = p.slot_bytes;
+    auto reg = [&](int k, uint32_t off) -> int64_t & {
+        return *reinterpret_cast<int64_t *>(lane_base + (uint32_t)k * kstride + off);
     };
+    const uint64_t stride = p.vlanes; // inputs handled per round of slots
 
-    unsigned long long s_steps = 0, s_out = 0, s_done = 0, s_q = 0, s_b = 0, s_ov = 0, s_os = 0;
-    uint64_t idx = gid;
-    bool active = idx < p.n;
-    uint32_t sb = 0, steps = 0;
-    // The next input of this lane is loaded one input ahead, so a refill
-    // never waits on HBM latency.
-    int32_t next_in = 0;
-    if (active) {
-        reg(p.in_reg) = sched_input(p, idx);
-        if (idx + p.lanes < p.n) next_in = sched_input(p, idx + p.lanes);
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0}; // steps, out, done, quiescent, budget, overflow, out-stop
+    uint64_t idx[K];
+    bool act[K];
+    uint32_t sb[K], steps[K];
+    int32_t nxt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        idx[k] = gid + (uint64_t)k * p.lanes;
+        act[k] = idx[k] < p.n;
+        sb[k] = 0;
+        steps[k] = 0;
+        nxt[k] = 0;
+        // the next input of each slot is loaded one input ahead, so a refill
+        // never waits on HBM latency
+        if (act[k]) {
+            reg(k, p.in_off) = sched_input(p, idx[k]);
+            if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
+        }
     }
 
     for (;;) {
-        const unsigned long long act = __ballot(active);
-        if (!act) break;
-        const int lead = __builtin_ctzll(act);
-        const uint32_t u = __builtin_amdgcn_readlane(sb, lead);
-        if (!(active && sb == u)) continue;
-        uint32_t pc = __builtin_amdgcn_readfirstlane(entry[__builtin_amdgcn_readfirstlane(u)]); // wave-uniform
-        bool done = false;
-        uint32_t st = 0;
-        int32_t outv = 0;
-        for (;;) {
-            const UOp I = fetch_uop(code, pc);
-            bool leave = false;
-            switch (I.op) {
-            case U_MOV: reg(I.d) = opnd(I.a, I.fl & UF_TA); pc += 1; break;
-            case U_LI: reg(I.d) = I.imm; pc += 1; break;
-            case U_ADD:
-                reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) + (uint64_t)opnd(I.b, I.fl & UF_TB));
-                pc += 1;
-                break;
-            case U_SUB:
-                reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) - (uint64_t)opnd(I.b, I.fl & UF_TB));
-                pc += 1;
-                break;
-            case U_ADDI: reg(I.d) = (int64_t)((uint64_t)opnd(I.a, I.fl & UF_TA) + (uint64_t)I.imm); pc += 1; break;
-            case U_RSUBI: reg(I.d) = (int64_t)((uint64_t)I.imm - (uint64_t)opnd(I.a, I.fl & UF_TA)); pc += 1; break;
-            case U_ST: p.slots[(uint64_t)I.imm * p.lanes + gid] = (int32_t)opnd(I.a, I.fl & UF_TA); pc += 1; break;
-            case U_STI:
-                p.slots[(uint64_t)((uint32_t)I.a | ((uint32_t)I.b << 16)) * p.lanes + gid] = (int32_t)I.imm;
-                pc += 1;
-                break;
-            case U_LD: reg(I.d) = p.slots[(uint64_t)I.imm * p.lanes + gid]; pc += 1; break;
-            case U_JUMP:
-                steps += (uint32_t)I.d | ((uint32_t)I.a << 16);
-                sb = (uint32_t)I.imm;
-                leave = true;
-                break;
-            case U_BR: {
-                const int64_t v = opnd(I.a, I.fl & UF_TA);
-                const uint32_t cond = (I.fl >> UF_COND_SHIFT) & 3u;
-                const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
-                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
-                sb = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
-                leave = true;
-                break;
-            }
-            case U_JRO: {
-                // IntClamp(ptr+v, 0, len-1) with an int64 wrapping add (program.go:354,362)
-                int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)opnd(I.a, I.fl & UF_TA));
-                t = t > (int64_t)I.b ? (int64_t)I.b : t;
-                t = t < 0 ? 0 : t;
-                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
-                sb = jtab[(uint64_t)I.imm + (uint64_t)t];
-                leave = true;
-                break;
-            }
-            case U_END:
-                steps += (uint32_t)fetch_uop(code, pc + 1).imm;
-                outv = (I.fl & UF_OUTREG) ? (int32_t)opnd(I.a, I.fl & UF_TA) : (int32_t)I.imm;
-                st = I.d;
-                done = true;
-                leave = true;
-                break;
-            case U_GUARD:
-                if ((uint64_t)steps + ((uint32_t)I.d | ((uint32_t)I.a << 16)) >= p.budget) {
-                    sb = (uint32_t)I.imm; // budget may be hit inside: take the checked variant
-                    leave = true;
-                }
-                pc += 1;
-                break;
-            case U_ROUND_END: {
-                const uint32_t c = (uint32_t)fetch_uop(code, pc + 1).imm;
-                if ((uint64_t)steps + c >= p.budget) {
-                    steps += c;
-                    outv = (I.fl & UF_OUTREG) ? (int32_t)opnd(I.a, I.fl & UF_TA) : (int32_t)I.imm;
-                    st = I.d;
-                    done = true;
-                    leave = true;
-                }
-                pc += 2;
-                break;
-            }
-            default: leave = true; done = true; st = 0; break; // corrupt stream: stop the lane
-            }
-            if (leave) break;
+        bool any = false;
+        uint32_t fsb = 0;
+#pragma unroll
+        for (int k = K - 1; k >= 0; --k) {
+            any = any || act[k];
+            if (act[k]) fsb = sb[k];
         }
-        if (done) {
-            const uint32_t reason = st & MK_ST_REASON_MASK;
-            p.out[idx] = (st & MK_ST_HAS_OUTPUT) ? outv : 0;
-            p.status[idx] = (uint8_t)st;
-            if (p.steps) p.steps[idx] = steps;
-            s_steps += steps;
-            s_out += (st & MK_ST_HAS_OUTPUT) != 0;
-            s_done += 1;
-            s_q += reason == MK_ST_QUIESCENT;
-            s_b += reason == MK_ST_BUDGET;
-            s_ov += reason == MK_ST_STACK_OVERFLOW;
-            s_os += reason == MK_ST_OUTPUT_STOP;
-            idx += p.lanes;
-            active = idx < p.n;
-            sb = 0;
-            steps = 0;
-            if (active) {
-                reg(p.in_reg) = next_in;
-                if (idx + p.lanes < p.n) next_in = sched_input(p, idx + p.lanes);
+        const unsigned long long anyb = __ballot(any);
+        if (!anyb) break;
+        const uint32_t u = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(fsb, __builtin_ctzll(anyb)));
+        bool mine[K], mine_any = false, mine_all = true;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            mine[k] = act[k] && sb[k] == u;
+            mine_any = mine_any || mine[k];
+            mine_all = mine_all && mine[k];
+        }
+        const bool full = __ballot(mine_any && !mine_all) == 0;
+        if (!mine_any) continue;
+        const uint32_t pc = __builtin_amdgcn_readfirstlane(entry[u]);
+        bool done[K];
+        uint32_t st[K];
+        int32_t outv[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            done[k] = false;
+            st[k] = 0;
+            outv[k] = 0;
+        }
+        if (u & 1u)
+            run_superblock<K, false, true>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
+        else if (full)
+            run_superblock<K, true, false>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
+        else
+            run_superblock<K, false, false>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!done[k]) continue;
+            const uint32_t reason = st[k] & MK_ST_REASON_MASK;
+            const bool has = (st[k] & MK_ST_HAS_OUTPUT) != 0;
+            p.out[idx[k]] = has ? outv[k] : 0;
+            p.status[idx[k]] = (uint8_t)st[k];
+            if (p.steps) p.steps[idx[k]] = steps[k];
+            cnt[0] += steps[k];
+            cnt[1] += has;
+            cnt[2] += 1;
+            cnt[3] += reason == MK_ST_QUIESCENT;
+            cnt[4] += reason == MK_ST_BUDGET;
+            cnt[5] += reason == MK_ST_STACK_OVERFLOW;
+            cnt[6] += reason == MK_ST_OUTPUT_STOP;
+            idx[k] += stride;
+            act[k] = idx[k] < p.n;
+            sb[k] = 0;
+            steps[k] = 0;
+            if (act[k]) {
+                reg(k, p.in_off) = nxt[k];
+                if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
             }
         }
     }
-
-    if (p.stats) {
-        const unsigned long long v0 = wave_sum(s_steps), v1 = wave_sum(s_out), v2 = wave_sum(s_done),
-                                 v3 = wave_sum(s_q), v4 = wave_sum(s_b), v5 = wave_sum(s_ov),
-                                 v6 = wave_sum(s_os);
-        if ((tid & 63) == 0 && v2) {
-            atomicAdd(&p.stats[0], v0);
-            atomicAdd(&p.stats[1], v1);
-            atomicAdd(&p.stats[2], v2);
-            if (v3) atomicAdd(&p.stats[3], v3);
-            if (v4) atomicAdd(&p.stats[4], v4);
-            if (v5) atomicAdd(&p.stats[5], v5);
-            if (v6) atomicAdd(&p.stats[6], v6);
-        }
-    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
 }
 
 __global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
@@ -585,7 +674,8 @@ __global__ void __launch_bounds__(kBlock) valu_probe(int iters, uint32_t *sink)
 // Host side
 // ------------------------------------------------------------------------
 struct SchedDev {
-    UOp *d_code = nullptr;
+    DOp *d_code = nullptr;
+    uint32_t block = 0;
     uint32_t *d_entry = nullptr;
     uint32_t *d_jtab = nullptr;
     int32_t *d_slots = nullptr;
@@ -610,6 +700,8 @@ struct DevCtx {
     size_t spill_bytes = 0;
     void *d_stage = nullptr; // host-API staging buffer
     size_t stage_bytes = 0;
+    unsigned long long *d_partials = nullptr; // per-wave counters
+    size_t partials_bytes = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -632,6 +724,7 @@ struct mk_net {
             (void)hipFree(c.d_code);
             (void)hipFree(c.d_spill);
             (void)hipFree(c.d_stage);
+            (void)hipFree(c.d_partials);
             for (auto &sc : sched) {
                 (void)hipFree(sc->dev[d].d_code);
                 (void)hipFree(sc->dev[d].d_entry);
@@ -758,15 +851,42 @@ int ensure_sched_device(SchedCache *sc, int d)
     if (sd.d_code) return MK_OK;
     DeviceGuard g(d);
     const SchedProgram &P = sc->prog;
-    const size_t cb = P.code.size() * sizeof(UOp), eb = P.entry.size() * 4, jb = std::max<size_t>(P.jtab.size(), 1) * 4;
+    sd.block = sched_block_size(P.nregs);
+    std::vector<uint32_t> entry;
+    const std::vector<DOp> code = assemble_device(P, sd.block, entry);
+    const size_t cb = code.size() * sizeof(DOp), eb = entry.size() * 4, jb = std::max<size_t>(P.jtab.size(), 1) * 4;
     if (hipMalloc(&sd.d_code, cb) != hipSuccess || hipMalloc(&sd.d_entry, eb) != hipSuccess ||
         hipMalloc(&sd.d_jtab, jb) != hipSuccess)
         return MK_ENOMEM;
-    if (hipMemcpy(sd.d_code, P.code.data(), cb, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(sd.d_entry, P.entry.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(sd.d_code, code.data(), cb, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(sd.d_entry, entry.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
         (!P.jtab.empty() && hipMemcpy(sd.d_jtab, P.jtab.data(), P.jtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
         return MK_EDEVICE;
     return MK_OK;
+}
+
+// Caller holds h->mu.  Per-wave counter buffer for `lanes` resident lanes.
+int ensure_partials(DevCtx &c, uint64_t lanes)
+{
+    const size_t need = (size_t)((lanes + 63) / 64) * 8 * sizeof(unsigned long long);
+    if (need <= c.partials_bytes) return MK_OK;
+    if (c.d_partials) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(c.d_partials);
+        c.d_partials = nullptr;
+        c.partials_bytes = 0;
+    }
+    if (hipMalloc(&c.d_partials, need) != hipSuccess) return MK_ENOMEM;
+    c.partials_bytes = need;
+    return MK_OK;
+}
+
+int launch_stats_reduce(DevCtx &c, uint64_t lanes, uint64_t *d_stats, hipStream_t stream)
+{
+    const uint32_t nwaves = (uint32_t)((lanes + 63) / 64);
+    hipLaunchKernelGGL(stats_reduce, dim3(1), dim3(256), 0, stream, (const unsigned long long *)c.d_partials, nwaves,
+                       reinterpret_cast<unsigned long long *>(d_stats));
+    return hipGetLastError() == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 
 // Caller holds h->mu.  Tier-2 launch; asynchronous on `stream`.
@@ -779,20 +899,26 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     SchedDev &sd = sc->dev[d];
     const SchedProgram &P = sc->prog;
     DeviceGuard g(d);
-    // LDS register file: nregs x 8 B per lane; keep <= 40 KiB per block.
-    int B = 256;
-    while (B > 64 && (size_t)P.nregs * B * 8 > 40 * 1024) B >>= 1;
-    const size_t lds = (size_t)P.nregs * B * 8;
+    // LDS register file: K slots x nregs x 8 B per thread (block size fixed by
+    // the assembly); as many slots as fit in 40 KiB per block, up to 4.
+    const int B = (int)sd.block;
+    const size_t slot_bytes = (size_t)P.nregs * B * 8;
+    int K = 4;
+    while (K > 1 && (size_t)K * slot_bytes > 40 * 1024) K >>= 1;
+    const size_t lds = (size_t)K * slot_bytes;
     if (lds > 160 * 1024) return MK_ELIMIT;
-    void *fn = reinterpret_cast<void *>(&tis_sched_exec);
+    void *fn = K == 4 ? reinterpret_cast<void *>(&tis_sched_exec<4>)
+             : K == 2 ? reinterpret_cast<void *>(&tis_sched_exec<2>)
+                      : reinterpret_cast<void *>(&tis_sched_exec<1>);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    const uint64_t want = (n + B - 1) / B;
+    const uint64_t want = (n + (uint64_t)B * K - 1) / ((uint64_t)B * K);
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(c.cus, 1);
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
     const uint64_t lanes = (uint64_t)blocks * B;
+    const uint64_t vlanes = lanes * (uint64_t)K;
     if (P.nslots) {
-        const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
+        const size_t need = (size_t)P.nslots * vlanes * sizeof(int32_t);
         if (need > sd.slots_bytes) {
             if (sd.d_slots) {
                 (void)hipDeviceSynchronize();
@@ -816,15 +942,18 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    p.stats = reinterpret_cast<unsigned long long *>(d_stats);
+    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = d_stats ? c.d_partials : nullptr;
     p.slots = sd.d_slots;
     p.lanes = lanes;
-    p.in_reg = P.in_reg;
-    const UOp *code = sd.d_code;
+    p.vlanes = vlanes;
+    p.in_off = P.in_reg * (uint32_t)B * 8;
+    p.slot_bytes = (uint32_t)slot_bytes;
+    const DOp *code = sd.d_code;
     const uint32_t *entry = sd.d_entry, *jtab = sd.d_jtab;
     void *args[] = {(void *)&code, (void *)&entry, (void *)&jtab, (void *)&p};
     if (hipLaunchKernel(fn, dim3(blocks), dim3(B), args, lds, stream) != hipSuccess) return MK_EDEVICE;
-    return MK_OK;
+    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
 }
 
 // Caller holds h->mu.  Asynchronous on `stream`.
@@ -877,7 +1006,8 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    p.stats = reinterpret_cast<unsigned long long *>(d_stats);
+    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = d_stats ? c.d_partials : nullptr;
     p.budget = budget;
     p.stack_cap = cap;
     p.flags = flags;
@@ -889,7 +1019,7 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     void *args[] = {(void *)&code, (void *)&p};
     if (hipLaunchKernel(L.fn, dim3(L.blocks), dim3(kBlock), args, L.lds, stream) != hipSuccess)
         return MK_EDEVICE;
-    return MK_OK;
+    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
 }
 
 void set_err(char *err, size_t len, const std::string &s)

@@ -54,8 +54,12 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
         return 1;
     }
     if (plan && plan_len) snprintf(plan, plan_len, "%s", mk::sched_disasm(P).c_str());
+    // execute the device form (block = 1: register byte offsets are r * 8)
+    std::vector<uint32_t> entry;
+    const std::vector<mk::DOp> D = mk::assemble_device(P, 1, entry);
     std::vector<int64_t> R(P.nregs);
     std::unordered_map<uint32_t, int32_t> slots;
+    auto reg = [&](uint32_t off) -> int64_t & { return R.at(off / 8); };
     for (size_t i = 0; i < n; i++) {
         std::fill(R.begin(), R.end(), (int64_t)0x5A5A5A5A5A5A5A5All); // stale register contents
         slots.clear();
@@ -65,71 +69,69 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
         bool done = false;
         uint64_t guard_words = 0;
         while (!done) {
-            uint32_t pc = P.entry[sb];
+            uint32_t pc = entry[sb];
             for (;;) {
                 if (++guard_words > (1ull << 34)) return -2; // runaway
-                const mk::UOp &I = P.code[pc];
+                const mk::DOp &I = D.at(pc);
                 bool leave = false;
                 const bool ta = I.fl & mk::UF_TA, tb = I.fl & mk::UF_TB;
                 switch (I.op) {
-                case mk::U_MOV: R[I.d] = sx(R[I.a], ta); pc++; break;
-                case mk::U_LI: R[I.d] = I.imm; pc++; break;
-                case mk::U_ADD: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) + (uint64_t)sx(R[I.b], tb)); pc++; break;
-                case mk::U_SUB: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) - (uint64_t)sx(R[I.b], tb)); pc++; break;
-                case mk::U_ADDI: R[I.d] = (int64_t)((uint64_t)sx(R[I.a], ta) + (uint64_t)I.imm); pc++; break;
-                case mk::U_RSUBI: R[I.d] = (int64_t)((uint64_t)I.imm - (uint64_t)sx(R[I.a], ta)); pc++; break;
-                case mk::U_ST: slots[(uint32_t)I.imm] = (int32_t)sx(R[I.a], ta); pc++; break;
-                case mk::U_STI: slots[(uint32_t)I.a | ((uint32_t)I.b << 16)] = (int32_t)I.imm; pc++; break;
+                case mk::U_MOV: reg(I.d) = sx(reg(I.a), ta); pc++; break;
+                case mk::U_LI: reg(I.d) = I.imm; pc++; break;
+                case mk::U_ADD: reg(I.d) = (int64_t)((uint64_t)sx(reg(I.a), ta) + (uint64_t)sx(reg(I.b), tb)); pc++; break;
+                case mk::U_SUB: reg(I.d) = (int64_t)((uint64_t)sx(reg(I.a), ta) - (uint64_t)sx(reg(I.b), tb)); pc++; break;
+                case mk::U_ADDI: reg(I.d) = (int64_t)((uint64_t)sx(reg(I.a), ta) + (uint64_t)I.imm); pc++; break;
+                case mk::U_RSUBI: reg(I.d) = (int64_t)((uint64_t)I.imm - (uint64_t)sx(reg(I.a), ta)); pc++; break;
+                case mk::U_ST: slots[(uint32_t)I.imm] = (int32_t)sx(reg(I.a), ta); pc++; break;
+                case mk::U_STI: slots[I.d] = (int32_t)I.imm; pc++; break;
                 case mk::U_LD: {
                     auto it = slots.find((uint32_t)I.imm);
                     if (it == slots.end()) return -3; // load of a slot never stored
-                    R[I.d] = it->second;
+                    reg(I.d) = it->second;
                     pc++;
                     break;
                 }
-                case mk::U_JUMP: steps += (uint32_t)I.d | ((uint32_t)I.a << 16); sb = (uint32_t)I.imm; leave = true; break;
+                case mk::U_JUMP: steps += I.inc; sb = (uint32_t)I.imm; leave = true; break;
                 case mk::U_BR: {
-                    const int64_t v = sx(R[I.a], ta);
+                    const int64_t v = sx(reg(I.a), ta);
                     const uint32_t c = (I.fl >> mk::UF_COND_SHIFT) & 3u;
                     const bool take = c == 0 ? v == 0 : c == 1 ? v != 0 : c == 2 ? v > 0 : v < 0;
-                    steps += (uint32_t)P.code[pc + 1].imm;
+                    steps += I.inc;
                     sb = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
                     leave = true;
                     break;
                 }
                 case mk::U_JRO: {
-                    int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)sx(R[I.a], ta));
+                    int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)sx(reg(I.a), ta));
                     t = t > (int64_t)I.b ? (int64_t)I.b : t;
                     t = t < 0 ? 0 : t;
-                    steps += (uint32_t)P.code[pc + 1].imm;
-                    sb = P.jtab[(size_t)I.imm + (size_t)t];
+                    steps += I.inc;
+                    sb = P.jtab.at((size_t)I.imm + (size_t)t);
                     leave = true;
                     break;
                 }
                 case mk::U_END:
-                    steps += (uint32_t)P.code[pc + 1].imm;
-                    outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(R[I.a], ta) : (int32_t)I.imm;
+                    steps += I.inc;
+                    outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(reg(I.a), ta) : (int32_t)I.imm;
                     st = I.d;
                     done = leave = true;
                     break;
                 case mk::U_GUARD:
-                    if ((uint64_t)steps + ((uint32_t)I.d | ((uint32_t)I.a << 16)) >= budget) {
+                    if ((uint64_t)steps + I.inc >= budget) {
                         sb = (uint32_t)I.imm;
                         leave = true;
                     }
                     pc++;
                     break;
-                case mk::U_ROUND_END: {
-                    const uint32_t c = (uint32_t)P.code[pc + 1].imm;
-                    if ((uint64_t)steps + c >= budget) {
-                        steps += c;
-                        outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(R[I.a], ta) : (int32_t)I.imm;
+                case mk::U_ROUND_END:
+                    if ((uint64_t)steps + I.inc >= budget) {
+                        steps += I.inc;
+                        outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(reg(I.a), ta) : (int32_t)I.imm;
                         st = I.d;
                         done = leave = true;
                     }
-                    pc += 2;
+                    pc++;
                     break;
-                }
                 default: return -4;
                 }
                 if (leave) break;

@@ -978,6 +978,58 @@ bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_outpu
     return c.run(out, why);
 }
 
+uint32_t sched_block_size(uint32_t nregs)
+{
+    // keep the LDS register file <= 40 KiB per block
+    uint32_t B = 256;
+    while (B > 64 && (size_t)nregs * B * 8 > 40 * 1024) B >>= 1;
+    return B;
+}
+
+std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t block, std::vector<uint32_t> &entry_out)
+{
+    std::vector<DOp> out;
+    std::vector<uint32_t> map(p.code.size() + 1, 0);
+    const uint32_t scale = block * 8;
+    for (size_t i = 0; i < p.code.size(); i++) {
+        map[i] = (uint32_t)out.size();
+        const UOp &u = p.code[i];
+        DOp o{};
+        o.op = u.op;
+        o.fl = u.fl;
+        o.imm = u.imm;
+        const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END;
+        const uint32_t ext = two ? (uint32_t)p.code[i + 1].imm : 0;
+        switch (u.op) {
+        case U_MOV: case U_ADDI: case U_RSUBI:
+            o.d = u.d * scale; o.a = u.a * scale; break;
+        case U_ADD: case U_SUB:
+            o.d = u.d * scale; o.a = u.a * scale; o.b = u.b * scale; break;
+        case U_LI: case U_LD:
+            o.d = u.d * scale; break;
+        case U_ST:
+            o.a = u.a * scale; break;
+        case U_STI:
+            o.d = (uint32_t)u.a | ((uint32_t)u.b << 16); break;
+        case U_JUMP: case U_GUARD:
+            o.inc = (uint32_t)u.d | ((uint32_t)u.a << 16); break;
+        case U_BR:
+            o.a = u.a * scale; o.inc = ext; break;
+        case U_JRO:
+            o.d = u.d; o.a = u.a * scale; o.b = u.b; o.inc = ext; break;
+        case U_END: case U_ROUND_END:
+            o.d = u.d; o.a = (u.fl & UF_OUTREG) ? u.a * scale : 0; o.inc = ext; break;
+        default: break;
+        }
+        out.push_back(o);
+        if (two) i++;
+    }
+    map[p.code.size()] = (uint32_t)out.size();
+    entry_out.resize(p.entry.size());
+    for (size_t v = 0; v < p.entry.size(); v++) entry_out[v] = map[p.entry[v]];
+    return out;
+}
+
 std::string sched_disasm(const SchedProgram &p)
 {
     static const char *names[U_COUNT] = {"MOV", "LI", "ADD", "SUB", "ADDI", "RSUBI", "ST", "STI",

@@ -74,6 +74,30 @@ struct SchedProgram {
     uint64_t sym_rounds = 0;     // rounds executed symbolically
 };
 
+// Device form of a micro-op (32 bytes = one s_load_dwordx8): every field is
+// pre-decoded into its own dword and register operands are LDS byte offsets
+// (reg * block * 8) for the block size the launch uses, so the kernel spends
+// no scalar instructions on decoding.  Two-word ops fold their extension
+// into `inc`.
+//   MOV/ADD/SUB/ADDI/RSUBI/LD/LI: d = dst offset, a/b = src offsets
+//   ST: a = src offset, imm = slot      STI: d = slot, imm = value
+//   JUMP: inc = steps, imm = target     GUARD: inc = max steps to a round end, imm = checked id
+//   BR: a = cond offset, imm = lo:taken hi:not-taken, inc = steps
+//   JRO: d = ip, a = operand offset, b = len-1, imm = jtab offset, inc = steps
+//   END/ROUND_END: d = status, a = out offset (UF_OUTREG) else imm, inc = steps
+struct DOp {
+    uint32_t op, fl, d, a, b, inc;
+    int64_t imm;
+};
+static_assert(sizeof(DOp) == 32, "DOp must be 32 bytes");
+
+// Assemble `p` for LDS blocks of `block` lanes.  entry_out[v] = first DOp of
+// superblock variant v.
+std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t block, std::vector<uint32_t> &entry_out);
+
+// LDS block size the executor uses for a program with `nregs` registers.
+uint32_t sched_block_size(uint32_t nregs);
+
 // Compile for the given stack capacity / stop-on-output option (both change
 // the control flow).  Returns false with a reason when a limit is exceeded;
 // the caller then uses the direct bytecode interpreter.
