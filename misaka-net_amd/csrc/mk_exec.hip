@@ -122,22 +122,24 @@ __device__ __forceinline__ void write_partials(unsigned long long *partials, uin
     }
 }
 
-// One block folds the per-wave partials into the caller's counters
-// (8 atomics per launch instead of 7 per wave on the same lines).
+// Folds the per-wave partials into the caller's counters: one thread per
+// wave partial, a block tree in LDS, then one atomic per counter per block.
 __global__ void __launch_bounds__(256) stats_reduce(const unsigned long long *__restrict__ partials,
                                                     uint32_t nwaves, unsigned long long *stats)
 {
-    __shared__ unsigned long long acc[256];
-    const uint32_t t = threadIdx.x, k = t & 7;
-    unsigned long long s = 0;
-    for (uint32_t w = t >> 3; w < nwaves; w += 32) s += partials[(size_t)w * 8 + k];
-    acc[t] = s;
+    __shared__ unsigned long long acc[8][256];
+    const uint32_t t = threadIdx.x, w = blockIdx.x * 256 + t;
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[k][t] = w < nwaves ? partials[(size_t)w * 8 + k] : 0ull;
     __syncthreads();
-    if (t < 8) {
-        unsigned long long tot = 0;
-        for (int g = 0; g < 32; g++) tot += acc[g * 8 + t];
-        if (tot) atomicAdd(&stats[t], tot);
+    for (uint32_t h = 128; h > 0; h >>= 1) {
+        if (t < h) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc[k][t] += acc[k][t + h];
+        }
+        __syncthreads();
     }
+    if (t < 8 && acc[t][0]) atomicAdd(&stats[t], acc[t][0]);
 }
 
 
@@ -884,8 +886,8 @@ int ensure_partials(DevCtx &c, uint64_t lanes)
 int launch_stats_reduce(DevCtx &c, uint64_t lanes, uint64_t *d_stats, hipStream_t stream)
 {
     const uint32_t nwaves = (uint32_t)((lanes + 63) / 64);
-    hipLaunchKernelGGL(stats_reduce, dim3(1), dim3(256), 0, stream, (const unsigned long long *)c.d_partials, nwaves,
-                       reinterpret_cast<unsigned long long *>(d_stats));
+    hipLaunchKernelGGL(stats_reduce, dim3((nwaves + 255) / 256), dim3(256), 0, stream,
+                       (const unsigned long long *)c.d_partials, nwaves, reinterpret_cast<unsigned long long *>(d_stats));
     return hipGetLastError() == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 
