@@ -392,28 +392,32 @@ struct SParams {
     int32_t *slots;      // [nslots][vlanes] stack slots in HBM
     uint64_t lanes;      // resident threads
     uint64_t vlanes;     // lanes * K (one input per slot)
-    uint32_t in_off;     // LDS byte offset of the input register within a slot
-    uint32_t slot_bytes; // LDS bytes of one slot's register file (nregs * block * 8)
+    uint32_t in_off;      // LDS byte offset of the input register (reg * K * B * 8)
+    uint32_t scratch_off; // LDS byte offset of a scratch register (writes of slots outside the group)
+    uint64_t scratch_slot; // HBM slot row for stores of slots outside the group
 };
 
 // `i` must be wave-uniform.  readfirstlane pins the index and every fetched
 // dword to SGPRs: the fetch is scalar loads and the opcode switch a scalar
 // branch (without it the compiler loses uniformity through the dispatch loop
 // and emits vector loads plus an exec-masked case chain).
+// readfirstlane returns a signed int: keep every word unsigned so that no
+// 32-bit half of an immediate is sign-extended into the other.
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
 __device__ __forceinline__ DOp fetch_dop(const DOp *__restrict__ code, uint32_t i)
 {
-    i = __builtin_amdgcn_readfirstlane(i);
+    i = rfl(i);
     const uint4 *q = reinterpret_cast<const uint4 *>(code) + 2 * (size_t)i;
     const uint4 w0 = q[0], w1 = q[1];
     DOp o;
-    o.op = __builtin_amdgcn_readfirstlane(w0.x);
-    o.fl = __builtin_amdgcn_readfirstlane(w0.y);
-    o.d = __builtin_amdgcn_readfirstlane(w0.z);
-    o.a = __builtin_amdgcn_readfirstlane(w0.w);
-    o.b = __builtin_amdgcn_readfirstlane(w1.x);
-    o.inc = __builtin_amdgcn_readfirstlane(w1.y);
-    o.imm = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane(w1.w) << 32) |
-                      (uint64_t)__builtin_amdgcn_readfirstlane(w1.z));
+    o.op = rfl(w0.x);
+    o.fl = rfl(w0.y);
+    o.d = rfl(w0.z);
+    o.a = rfl(w0.w);
+    o.b = rfl(w1.x);
+    o.inc = rfl(w1.y);
+    o.imm = (int64_t)(((uint64_t)rfl(w1.w) << 32) | (uint64_t)rfl(w1.z));
     return o;
 }
 
@@ -424,143 +428,217 @@ __device__ __forceinline__ int32_t sched_input(const SParams &p, uint64_t i)
     return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
 }
 
-// Runs superblock micro-ops from `pc` for the slots flagged in `mine` until
-// the group exits.  FULL: every thread taking part has all K slots in the
-// group, so no per-slot masking is emitted.  CHECKED: the budget-checked
-// variant, where ROUND_END can end single slots.
-template <int K, bool FULL, bool CHECKED>
-__device__ __forceinline__ void run_superblock(const DOp *__restrict__ code, const uint32_t *__restrict__ jtab,
-                                               const SParams &p, char *lane_base, uint32_t kstride,
-                                               uint64_t vlane0, uint32_t pc, bool (&mine)[K], uint32_t (&sb)[K],
-                                               uint32_t (&steps)[K], bool (&done)[K], uint32_t (&st)[K],
-                                               int32_t (&outv)[K])
+// ---- tier-2 superblock execution ------------------------------------------
+// LDS register file layout: [reg][slot k][lane] int64, so register r of slot k
+// for this lane sits at lane_base + r * (K * B * 8) + k * (B * 8).  DOp register
+// operands are pre-scaled byte offsets r * K * B * 8 (assemble_device); with B
+// a template constant the K slots of one register are one address computation
+// plus immediate-offset ds_read/ds_write.
+
+template <int K, int B>
+struct Slots {
+    char *lane_base;
+    __device__ __forceinline__ int64_t *at(uint32_t off) const { return reinterpret_cast<int64_t *>(lane_base + off); }
+};
+
+__device__ __forceinline__ int64_t sx32(int64_t v, uint32_t t) { return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v; }
+
+// Executes data micro-ops (MOV..LD) from `pc` and returns the first control
+// op, leaving `pc` on it.  The loop carries nothing but `pc`.  FULL: every
+// slot of the thread is in the group.  Otherwise slots outside the group
+// compute too (reading stale registers is harmless) but their writes go to a
+// scratch register / scratch HBM row -- selects instead of per-slot branches,
+// so the loop never manipulates the exec mask.
+template <int K, int B>
+__device__ __forceinline__ void load_slots(const Slots<K, B> &S, uint32_t off, uint32_t t, int64_t (&v)[K])
 {
-    auto reg = [&](int k, uint32_t off) -> int64_t & {
-        return *reinterpret_cast<int64_t *>(lane_base + (uint32_t)k * kstride + off);
-    };
-    auto opnd = [&](int k, uint32_t off, uint32_t t) -> int64_t {
-        const int64_t v = reg(k, off);
-        return t ? (int64_t)(int32_t)(uint32_t)(uint64_t)v : v;
-    };
-    // HBM stack slots are [slot][virtual lane], virtual lane = k * lanes + gid
-    auto slot = [&](int k, uint64_t s) -> int32_t & {
-        return p.slots[s * p.vlanes + vlane0 + (uint64_t)k * p.lanes];
-    };
-#define MK_SLOTS for (int k = 0; k < K; ++k) if (FULL || mine[k])
+    const int64_t *a = S.at(off);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = a[k * B];
+    if (t) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = (int64_t)(int32_t)(uint32_t)(uint64_t)v[k];
+    }
+}
+
+template <int K, int B, bool FULL>
+__device__ __forceinline__ DOp run_data(const DOp *__restrict__ code, uint32_t &pc, const SParams &p,
+                                        const Slots<K, B> &S, uint64_t vlane0, const bool (&mine)[K])
+{
     for (;;) {
         const DOp I = fetch_dop(code, pc);
-        const uint32_t ta = I.fl & UF_TA, tb = I.fl & UF_TB;
-        bool leave = false;
-        // ordered by frequency in compiled schedules (the scalar unit is the
-        // bottleneck: a hot op should cost one compare)
-        if (I.op == U_ADDI) {
-            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) + (uint64_t)I.imm);
-        } else if (I.op == U_MOV) {
-            MK_SLOTS reg(k, I.d) = opnd(k, I.a, ta);
-        } else if (I.op == U_BR) {
-            const uint32_t cond = (I.fl >> UF_COND_SHIFT) & 3u;
-            MK_SLOTS {
-                const int64_t v = opnd(k, I.a, ta);
-                const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
-                steps[k] += I.inc;
-                sb[k] = take ? (uint32_t)(uint64_t)I.imm : (uint32_t)((uint64_t)I.imm >> 32);
-            }
-            leave = true;
-        } else if (I.op == U_END) {
-            MK_SLOTS {
-                steps[k] += I.inc;
-                outv[k] = (I.fl & UF_OUTREG) ? (int32_t)opnd(k, I.a, ta) : (int32_t)I.imm;
-                st[k] = I.d;
-                done[k] = true;
-            }
-            leave = true;
-        } else if (I.op == U_JUMP) {
-            MK_SLOTS {
-                steps[k] += I.inc;
-                sb[k] = (uint32_t)I.imm;
-            }
-            leave = true;
-        } else if (!CHECKED && I.op == U_GUARD) {
-            // any slot that could reach the budget inside: the whole group
-            // takes the checked variant (exact for every slot)
-            bool need = false;
-            MK_SLOTS need = need || (uint64_t)steps[k] + I.inc >= p.budget;
-            if (__ballot(need)) {
-                MK_SLOTS sb[k] = (uint32_t)I.imm;
-                leave = true;
-            }
-        } else if (I.op == U_ADD) {
-            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) + (uint64_t)opnd(k, I.b, tb));
-        } else if (I.op == U_SUB) {
-            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)opnd(k, I.a, ta) - (uint64_t)opnd(k, I.b, tb));
-        } else if (I.op == U_RSUBI) {
-            MK_SLOTS reg(k, I.d) = (int64_t)((uint64_t)I.imm - (uint64_t)opnd(k, I.a, ta));
-        } else if (I.op == U_LD) {
-            MK_SLOTS reg(k, I.d) = slot(k, (uint64_t)I.imm);
-        } else if (I.op == U_ST) {
-            MK_SLOTS slot(k, (uint64_t)I.imm) = (int32_t)opnd(k, I.a, ta);
-        } else if (I.op == U_LI) {
-            MK_SLOTS reg(k, I.d) = I.imm;
-        } else if (I.op == U_STI) {
-            MK_SLOTS slot(k, I.d) = (int32_t)I.imm;
-        } else if (I.op == U_JRO) {
-            MK_SLOTS {
-                // IntClamp(ptr+v, 0, len-1) with an int64 wrapping add (program.go:354,362)
-                int64_t t = (int64_t)((uint64_t)I.d + (uint64_t)opnd(k, I.a, ta));
-                t = t > (int64_t)I.b ? (int64_t)I.b : t;
-                t = t < 0 ? 0 : t;
-                steps[k] += I.inc;
-                sb[k] = jtab[(uint64_t)I.imm + (uint64_t)t];
-            }
-            leave = true;
-        } else if (CHECKED && I.op == U_ROUND_END) {
-            bool left = false;
-            MK_SLOTS {
-                if ((uint64_t)steps[k] + I.inc >= p.budget) {
-                    steps[k] += I.inc;
-                    outv[k] = (I.fl & UF_OUTREG) ? (int32_t)opnd(k, I.a, ta) : (int32_t)I.imm;
-                    st[k] = I.d;
-                    done[k] = true;
-                    mine[k] = false;
+        if (I.op > U_LD) return I;
+        if (I.op <= U_RSUBI) { // MOV LI ADD SUB ADDI RSUBI: int64 arithmetic on registers
+            int64_t v[K];
+            if (I.op == U_LI) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) v[k] = I.imm;
+            } else {
+                load_slots<K, B>(S, I.a, I.fl & UF_TA, v);
+                if (I.op == U_ADDI) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) v[k] = (int64_t)((uint64_t)v[k] + (uint64_t)I.imm);
+                } else if (I.op == U_RSUBI) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) v[k] = (int64_t)((uint64_t)I.imm - (uint64_t)v[k]);
+                } else if (I.op != U_MOV) {
+                    int64_t w[K];
+                    load_slots<K, B>(S, I.b, I.fl & UF_TB, w);
+                    if (I.op == U_ADD) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) v[k] = (int64_t)((uint64_t)v[k] + (uint64_t)w[k]);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) v[k] = (int64_t)((uint64_t)v[k] - (uint64_t)w[k]);
+                    }
                 }
-                left = left || mine[k];
             }
-            if (!__ballot(left)) leave = true; // every slot of the group stopped here
-        } else {
-            MK_SLOTS { // corrupt stream: end the slots
-                st[k] = 0;
-                done[k] = true;
+            if (FULL) {
+                int64_t *d = S.at(I.d);
+#pragma unroll
+                for (int k = 0; k < K; ++k) d[k * B] = v[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) S.at(mine[k] ? I.d : p.scratch_off)[k * B] = v[k];
             }
-            leave = true;
+        } else if (I.op == U_LD) { // stack entry back from its HBM slot
+            const int32_t *src = p.slots + (uint64_t)I.imm * p.vlanes + vlane0;
+            int64_t v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) v[k] = src[(uint64_t)k * p.lanes];
+            if (FULL) {
+                int64_t *d = S.at(I.d);
+#pragma unroll
+                for (int k = 0; k < K; ++k) d[k * B] = v[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) S.at(mine[k] ? I.d : p.scratch_off)[k * B] = v[k];
+            }
+        } else { // ST / STI: stack entry to its HBM slot
+            int64_t v[K];
+            uint64_t slot;
+            if (I.op == U_STI) {
+                slot = I.d;
+#pragma unroll
+                for (int k = 0; k < K; ++k) v[k] = I.imm;
+            } else {
+                slot = (uint32_t)I.imm;
+                load_slots<K, B>(S, I.a, I.fl & UF_TA, v);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint64_t row = (FULL || mine[k]) ? slot : p.scratch_slot;
+                p.slots[row * p.vlanes + vlane0 + (uint64_t)k * p.lanes] = (int32_t)v[k];
+            }
         }
-        if (leave) break;
         ++pc;
     }
-#undef MK_SLOTS
+}
+
+// Applies control op E (JUMP/BR/JRO/END) to the slots in `mine` (selects).
+template <int K, int B>
+__device__ __forceinline__ void apply_exit(const DOp &E, const uint32_t *__restrict__ jtab, const Slots<K, B> &S,
+                                           const bool (&mine)[K], uint32_t (&sb)[K], uint32_t (&steps)[K],
+                                           bool (&done)[K], uint32_t (&st)[K], int32_t (&outv)[K])
+{
+    const uint32_t ta = E.fl & UF_TA;
+    const int64_t *a = S.at(E.a);
+    if (E.op == U_JUMP) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            steps[k] += mine[k] ? E.inc : 0u;
+            sb[k] = mine[k] ? (uint32_t)E.imm : sb[k];
+        }
+    } else if (E.op == U_BR) {
+        const uint32_t cond = (E.fl >> UF_COND_SHIFT) & 3u;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t v = sx32(a[k * B], ta);
+            const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
+            steps[k] += mine[k] ? E.inc : 0u;
+            const uint32_t nsb = take ? (uint32_t)(uint64_t)E.imm : (uint32_t)((uint64_t)E.imm >> 32);
+            sb[k] = mine[k] ? nsb : sb[k];
+        }
+    } else if (E.op == U_END) {
+        const bool outreg = (E.fl & UF_OUTREG) != 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            steps[k] += mine[k] ? E.inc : 0u;
+            const int32_t o = outreg ? (int32_t)sx32(a[k * B], ta) : (int32_t)E.imm;
+            outv[k] = mine[k] ? o : outv[k];
+            st[k] = mine[k] ? E.d : st[k];
+            done[k] = done[k] || mine[k];
+        }
+    } else if (E.op == U_JRO) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            // IntClamp(ptr+v, 0, len-1) with an int64 wrapping add (program.go:354,362)
+            int64_t t = (int64_t)((uint64_t)E.d + (uint64_t)sx32(a[k * B], ta));
+            t = t > (int64_t)E.b ? (int64_t)E.b : t;
+            t = t < 0 ? 0 : t;
+            steps[k] += mine[k] ? E.inc : 0u;
+            if (mine[k]) sb[k] = jtab[(uint64_t)E.imm + (uint64_t)t];
+        }
+    } else { // corrupt stream: end the slots
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            st[k] = mine[k] ? 0u : st[k];
+            done[k] = done[k] || mine[k];
+        }
+    }
+}
+
+// Budget-checked variant (taken only by groups that could reach the budget
+// inside a superblock): ROUND_END may stop single slots.
+template <int K, int B>
+__device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__restrict__ jtab, uint32_t pc,
+                            const SParams &p, const Slots<K, B> &S, uint64_t vlane0, bool (&mine)[K],
+                            uint32_t (&sb)[K], uint32_t (&steps)[K], bool (&done)[K], uint32_t (&st)[K],
+                            int32_t (&outv)[K])
+{
+    for (;;) {
+        const DOp E = run_data<K, B, false>(code, pc, p, S, vlane0, mine);
+        if (E.op == U_ROUND_END) {
+            const int64_t *a = S.at(E.a);
+            bool left = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool stop = mine[k] && (uint64_t)steps[k] + E.inc >= p.budget;
+                const int32_t o = (E.fl & UF_OUTREG) ? (int32_t)sx32(a[k * B], E.fl & UF_TA) : (int32_t)E.imm;
+                steps[k] += stop ? E.inc : 0u;
+                outv[k] = stop ? o : outv[k];
+                st[k] = stop ? E.d : st[k];
+                done[k] = done[k] || stop;
+                mine[k] = mine[k] && !stop;
+                left = left || mine[k];
+            }
+            if (!__ballot(left)) return;
+            ++pc;
+            continue;
+        }
+        apply_exit<K, B>(E, jtab, S, mine, sb, steps, done, st, outv);
+        return;
+    }
 }
 
 // Tier-2 kernel: each thread carries K independent inputs ("slots"); one
 // scalar fetch + dispatch of a micro-op serves all K x 64 of them.
-template <int K>
-__global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__ code,
-                                                         const uint32_t *__restrict__ entry,
-                                                         const uint32_t *__restrict__ jtab, SParams p)
+template <int K, int B>
+__global__ void __launch_bounds__(B) tis_sched_exec(const DOp *__restrict__ code, const uint32_t *__restrict__ entry,
+                                                    const uint32_t *__restrict__ jtab, SParams p)
 {
-    extern __shared__ int64_t R[]; // [K][nregs][blockDim.x] 64-bit registers
+    extern __shared__ int64_t R[]; // [nregs][K][B]
     const uint32_t tid = threadIdx.x;
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + tid;
-    char *const lane_base = reinterpret_cast<char *>(R) + tid * 8;
-    const uint32_t kstride = p.slot_bytes;
-    auto reg = [&](int k, uint32_t off) -> int64_t & {
-        return *reinterpret_cast<int64_t *>(lane_base + (uint32_t)k * kstride + off);
-    };
-    const uint64_t stride = p.vlanes; // inputs handled per round of slots
+    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
+    const Slots<K, B> S{reinterpret_cast<char *>(R) + tid * 8};
+    const uint64_t stride = p.vlanes; // inputs per round of all slots
 
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0}; // steps, out, done, quiescent, budget, overflow, out-stop
     uint64_t idx[K];
     bool act[K];
     uint32_t sb[K], steps[K];
     int32_t nxt[K];
+    int64_t *in_reg = S.at(p.in_off);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         idx[k] = gid + (uint64_t)k * p.lanes;
@@ -571,7 +649,7 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__
         // the next input of each slot is loaded one input ahead, so a refill
         // never waits on HBM latency
         if (act[k]) {
-            reg(k, p.in_off) = sched_input(p, idx[k]);
+            in_reg[k * B] = sched_input(p, idx[k]);
             if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
         }
     }
@@ -586,7 +664,7 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__
         }
         const unsigned long long anyb = __ballot(any);
         if (!anyb) break;
-        const uint32_t u = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(fsb, __builtin_ctzll(anyb)));
+        const uint32_t u = rfl((uint32_t)__builtin_amdgcn_readlane((int)fsb, __builtin_ctzll(anyb)));
         bool mine[K], mine_any = false, mine_all = true;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -596,7 +674,7 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__
         }
         const bool full = __ballot(mine_any && !mine_all) == 0;
         if (!mine_any) continue;
-        const uint32_t pc = __builtin_amdgcn_readfirstlane(entry[u]);
+        uint32_t pc = rfl(entry[u]);
         bool done[K];
         uint32_t st[K];
         int32_t outv[K];
@@ -606,12 +684,31 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__
             st[k] = 0;
             outv[k] = 0;
         }
-        if (u & 1u)
-            run_superblock<K, false, true>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
-        else if (full)
-            run_superblock<K, true, false>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
-        else
-            run_superblock<K, false, false>(code, jtab, p, lane_base, kstride, gid, pc, mine, sb, steps, done, st, outv);
+        if (u & 1u) {
+            run_checked<K, B>(code, jtab, pc, p, S, gid, mine, sb, steps, done, st, outv);
+        } else {
+            for (;;) {
+                const DOp E = full ? run_data<K, B, true>(code, pc, p, S, gid, mine)
+                                   : run_data<K, B, false>(code, pc, p, S, gid, mine);
+                if (E.op == U_GUARD) {
+                    // any slot that could reach the budget inside: the whole
+                    // group takes the checked variant (exact for every slot)
+                    bool need = false;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) need = need || (mine[k] && (uint64_t)steps[k] + E.inc >= p.budget);
+                    if (__ballot(need)) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            if (mine[k]) sb[k] = (uint32_t)E.imm;
+                        break;
+                    }
+                    ++pc;
+                    continue;
+                }
+                apply_exit<K, B>(E, jtab, S, mine, sb, steps, done, st, outv);
+                break;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (!done[k]) continue;
@@ -632,7 +729,7 @@ __global__ void __launch_bounds__(kBlock) tis_sched_exec(const DOp *__restrict__
             sb[k] = 0;
             steps[k] = 0;
             if (act[k]) {
-                reg(k, p.in_off) = nxt[k];
+                in_reg[k * B] = nxt[k];
                 if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
             }
         }
@@ -677,7 +774,7 @@ __global__ void __launch_bounds__(kBlock) valu_probe(int iters, uint32_t *sink)
 // ------------------------------------------------------------------------
 struct SchedDev {
     DOp *d_code = nullptr;
-    uint32_t block = 0;
+    uint32_t block = 0, slots = 0;
     uint32_t *d_entry = nullptr;
     uint32_t *d_jtab = nullptr;
     int32_t *d_slots = nullptr;
@@ -846,6 +943,27 @@ SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
     return h->sched.back().get();
 }
 
+// Launch geometry of the tier-2 kernel for a program with `nregs` registers:
+// block size B and K input slots per thread, LDS nregs*K*B*8 <= 40 KiB.
+void sched_geometry(uint32_t nregs, uint32_t &B, uint32_t &K)
+{
+    const size_t r = (size_t)nregs + 1; // + scratch register
+    B = 256;
+    while (B > 64 && r * B * 8 > 40 * 1024) B >>= 1;
+    K = 4;
+    while (K > 1 && r * K * B * 8 > 40 * 1024) K >>= 1;
+}
+
+void *sched_kernel(int K, int B)
+{
+    if (B == 256 && K == 4) return reinterpret_cast<void *>(&tis_sched_exec<4, 256>);
+    if (B == 256 && K == 2) return reinterpret_cast<void *>(&tis_sched_exec<2, 256>);
+    if (B == 256 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 256>);
+    if (B == 128 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 128>);
+    if (B == 64 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 64>);
+    return nullptr;
+}
+
 // Caller holds h->mu.
 int ensure_sched_device(SchedCache *sc, int d)
 {
@@ -853,9 +971,9 @@ int ensure_sched_device(SchedCache *sc, int d)
     if (sd.d_code) return MK_OK;
     DeviceGuard g(d);
     const SchedProgram &P = sc->prog;
-    sd.block = sched_block_size(P.nregs);
+    sched_geometry(P.nregs, sd.block, sd.slots);
     std::vector<uint32_t> entry;
-    const std::vector<DOp> code = assemble_device(P, sd.block, entry);
+    const std::vector<DOp> code = assemble_device(P, sd.block * sd.slots * 8, entry);
     const size_t cb = code.size() * sizeof(DOp), eb = entry.size() * 4, jb = std::max<size_t>(P.jtab.size(), 1) * 4;
     if (hipMalloc(&sd.d_code, cb) != hipSuccess || hipMalloc(&sd.d_entry, eb) != hipSuccess ||
         hipMalloc(&sd.d_jtab, jb) != hipSuccess)
@@ -901,17 +1019,13 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     SchedDev &sd = sc->dev[d];
     const SchedProgram &P = sc->prog;
     DeviceGuard g(d);
-    // LDS register file: K slots x nregs x 8 B per thread (block size fixed by
-    // the assembly); as many slots as fit in 40 KiB per block, up to 4.
-    const int B = (int)sd.block;
-    const size_t slot_bytes = (size_t)P.nregs * B * 8;
-    int K = 4;
-    while (K > 1 && (size_t)K * slot_bytes > 40 * 1024) K >>= 1;
-    const size_t lds = (size_t)K * slot_bytes;
+    // LDS register file [nregs][K][B] x 8 B; block size and slot count are
+    // fixed by the assembly (sched_geometry).
+    const int B = (int)sd.block, K = (int)sd.slots;
+    const size_t lds = (size_t)(P.nregs + 1) * K * B * 8; // + one scratch register
     if (lds > 160 * 1024) return MK_ELIMIT;
-    void *fn = K == 4 ? reinterpret_cast<void *>(&tis_sched_exec<4>)
-             : K == 2 ? reinterpret_cast<void *>(&tis_sched_exec<2>)
-                      : reinterpret_cast<void *>(&tis_sched_exec<1>);
+    void *fn = sched_kernel(K, B);
+    if (!fn) return MK_ELIMIT;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     const uint64_t want = (n + (uint64_t)B * K - 1) / ((uint64_t)B * K);
@@ -920,7 +1034,7 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     const uint64_t lanes = (uint64_t)blocks * B;
     const uint64_t vlanes = lanes * (uint64_t)K;
     if (P.nslots) {
-        const size_t need = (size_t)P.nslots * vlanes * sizeof(int32_t);
+        const size_t need = (size_t)(P.nslots + 1) * vlanes * sizeof(int32_t); // + scratch row
         if (need > sd.slots_bytes) {
             if (sd.d_slots) {
                 (void)hipDeviceSynchronize();
@@ -949,8 +1063,9 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     p.slots = sd.d_slots;
     p.lanes = lanes;
     p.vlanes = vlanes;
-    p.in_off = P.in_reg * (uint32_t)B * 8;
-    p.slot_bytes = (uint32_t)slot_bytes;
+    p.in_off = P.in_reg * (uint32_t)(K * B * 8);
+    p.scratch_off = P.nregs * (uint32_t)(K * B * 8);
+    p.scratch_slot = P.nslots;
     const DOp *code = sd.d_code;
     const uint32_t *entry = sd.d_entry, *jtab = sd.d_jtab;
     void *args[] = {(void *)&code, (void *)&entry, (void *)&jtab, (void *)&p};

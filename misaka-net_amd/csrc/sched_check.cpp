@@ -54,9 +54,9 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
         return 1;
     }
     if (plan && plan_len) snprintf(plan, plan_len, "%s", mk::sched_disasm(P).c_str());
-    // execute the device form (block = 1: register byte offsets are r * 8)
+    // execute the device form (one lane, one slot: register byte offsets are r * 8)
     std::vector<uint32_t> entry;
-    const std::vector<mk::DOp> D = mk::assemble_device(P, 1, entry);
+    const std::vector<mk::DOp> D = mk::assemble_device(P, 8, entry);
     std::vector<int64_t> R(P.nregs);
     std::unordered_map<uint32_t, int32_t> slots;
     auto reg = [&](uint32_t off) -> int64_t & { return R.at(off / 8); };

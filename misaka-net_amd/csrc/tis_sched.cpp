@@ -978,19 +978,11 @@ bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_outpu
     return c.run(out, why);
 }
 
-uint32_t sched_block_size(uint32_t nregs)
-{
-    // keep the LDS register file <= 40 KiB per block
-    uint32_t B = 256;
-    while (B > 64 && (size_t)nregs * B * 8 > 40 * 1024) B >>= 1;
-    return B;
-}
-
-std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t block, std::vector<uint32_t> &entry_out)
+std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std::vector<uint32_t> &entry_out)
 {
     std::vector<DOp> out;
     std::vector<uint32_t> map(p.code.size() + 1, 0);
-    const uint32_t scale = block * 8;
+    const uint32_t scale = reg_bytes;
     for (size_t i = 0; i < p.code.size(); i++) {
         map[i] = (uint32_t)out.size();
         const UOp &u = p.code[i];

@@ -76,7 +76,7 @@ struct SchedProgram {
 
 // Device form of a micro-op (32 bytes = one s_load_dwordx8): every field is
 // pre-decoded into its own dword and register operands are LDS byte offsets
-// (reg * block * 8) for the block size the launch uses, so the kernel spends
+// (reg * stride) for the layout the launch uses, so the kernel spends
 // no scalar instructions on decoding.  Two-word ops fold their extension
 // into `inc`.
 //   MOV/ADD/SUB/ADDI/RSUBI/LD/LI: d = dst offset, a/b = src offsets
@@ -91,12 +91,10 @@ struct DOp {
 };
 static_assert(sizeof(DOp) == 32, "DOp must be 32 bytes");
 
-// Assemble `p` for LDS blocks of `block` lanes.  entry_out[v] = first DOp of
-// superblock variant v.
-std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t block, std::vector<uint32_t> &entry_out);
-
-// LDS block size the executor uses for a program with `nregs` registers.
-uint32_t sched_block_size(uint32_t nregs);
+// Assemble `p` with register operands scaled to `reg_bytes` (the byte stride
+// between consecutive registers in the executor's LDS layout).  entry_out[v]
+// = first DOp of superblock variant v.
+std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std::vector<uint32_t> &entry_out);
 
 // Compile for the given stack capacity / stop-on-output option (both change
 // the control flow).  Returns false with a reason when a limit is exceeded;

@@ -220,3 +220,14 @@ def test_c3_64m_shard_properties(gpu, interp):
         if cls.any():
             i = int(np.nonzero(cls)[0][0])
             assert (sp[cls] == oracle(nodes, x[i:i + 1])[2][0]).all()
+
+
+@pytest.mark.parametrize("interp", TIERS)
+def test_wide_immediates_on_symbolic_acc(gpu, interp):
+    # immediates whose low 32-bit word has bit 31 set, applied to a data-dependent ACC
+    prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
+            "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
+            "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
+    nodes = [("n", "program", prog)]
+    xs = po.gen_inputs(SEED, 4096)
+    assert_same(mk.Network(nodes).compute_batch(xs, interp=interp), oracle(nodes, xs), "wide imm")

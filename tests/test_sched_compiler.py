@@ -68,3 +68,10 @@ def test_random_networks():
         except sc.NotCompiled:
             declined += 1
     assert declined < 30
+
+
+def test_wide_immediates_on_symbolic_acc():
+    prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
+            "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
+            "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
+    same([("n", "program", prog)], po.gen_inputs(SEED, 500))
