@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=0, help="lanes per GPU (default: the config's)")
     ap.add_argument("--gather", action="store_true", help="also time an ordered RCCL gather of outputs to rank 0")
     ap.add_argument("--interp", action="store_true", help="force the tier-1 bytecode interpreter")
+    ap.add_argument("--gen-inputs", action="store_true",
+                    help="diagnostic: generate inputs inside the executor instead of reading them from HBM")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -142,7 +144,8 @@ def main():
 
     def step(stats_ptr):
         net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats_ptr,
-                           in_ptr=x.data_ptr(), in_kind=N.MK_IN_I32, device=dev, stream=sh, interp=args.interp)
+                           in_ptr=None if args.gen_inputs else x.data_ptr(), in_kind=N.MK_IN_I32, seed=SEED,
+                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, interp=args.interp)
 
     for _ in range(args.warmup):
         step(None)
@@ -193,7 +196,7 @@ def main():
             log("valu probe failed:", e)
     peak = max(SPEC_LANE_OPS, peak_meas or 0.0)
     achieved = K_LANE_OPS * per_gpu_kernel_rate
-    bytes_per_lane = 4 + 4 + 1  # int32 input read, int32 out + u8 status written
+    bytes_per_lane = (0 if args.gen_inputs else 4) + 4 + 1  # int32 input read, int32 out + u8 status written
     hbm_achieved = bytes_per_lane * lanes * args.steps / kern_max
 
     if rank == 0:
