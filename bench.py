@@ -102,12 +102,16 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per GPU (default: the config's)")
     ap.add_argument("--gather", action="store_true", help="also time an ordered RCCL gather of outputs to rank 0")
-    ap.add_argument("--interp", action="store_true", help="force the tier-1 bytecode interpreter")
+    ap.add_argument("--interp", action="store_true", help="force the tier-1 bytecode interpreter (= --mode interp)")
+    ap.add_argument("--mode", default=None, choices=["jit", "tile", "refill", "interp"],
+                    help="force an executor mode (default: automatic)")
     ap.add_argument("--gen-inputs", action="store_true",
                     help="diagnostic: generate inputs inside the executor instead of reading them from HBM")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
+    if args.interp:
+        args.mode = "interp"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -145,8 +149,9 @@ def main():
     def step(stats_ptr):
         net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats_ptr,
                            in_ptr=None if args.gen_inputs else x.data_ptr(), in_kind=N.MK_IN_I32, seed=SEED,
-                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, interp=args.interp)
+                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, mode=args.mode)
 
+    net.prepare(mode=args.mode, device=dev)  # schedule + native kernel compiled before any timing
     for _ in range(args.warmup):
         step(None)
     torch.cuda.synchronize()
@@ -222,7 +227,7 @@ def main():
                 "global_lanes": lanes * world,
                 "network": args.config,
                 "parallelism": f"dp{world} (contiguous lane shards, no data-path collective)",
-                "executor": net.plan(interp=args.interp),
+                "executor": net.plan(mode=args.mode),
             },
             "results_per_s": with_out / wall_max,
             "node_instr_per_lane": retired / (lanes * world * args.steps),

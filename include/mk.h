@@ -66,6 +66,20 @@ typedef struct {
  * micro-ops (tier 2); networks the compiler cannot bound fall back to
  * tier 1 automatically.  Both tiers give identical results. */
 #define MK_FLAG_FORCE_INTERP 2u
+/* Select the tier-2 superblock interpreter with the given lane scheduling
+ * (results are identical either way; tier 2's default is TILE).  TILE: every
+ * thread owns K contiguous inputs of a tile and the tile is written back with
+ * vector stores once all of its lanes finished.  REFILL: a finished slot
+ * immediately takes the next input. */
+#define MK_FLAG_TILE 4u
+#define MK_FLAG_REFILL 8u
+/* Tier 3: the compiled schedule as a native gfx950 kernel generated and
+ * compiled (hiprtc) once per network and option set.  Used by default when
+ * the schedule fits its limits; MK_FLAG_JIT demands it (MK_ELIMIT when it is
+ * unavailable -- mk_net_plan gives the reason), MK_FLAG_TILE / MK_FLAG_REFILL
+ * select the tier-2 superblock interpreter, MK_FLAG_FORCE_INTERP tier 1.
+ * MK_JIT=0 in the environment disables tier 3. */
+#define MK_FLAG_JIT 16u
 
 typedef struct {
     uint32_t budget;      /* retired node-instructions per lane; 0 = 1<<20          */
@@ -139,9 +153,20 @@ int mk_tokenize(const char *program, char *out, size_t out_len);
 int mk_net_disasm(const mk_net *net, char *out, size_t out_len);
 
 /* Which tier `opts` selects for this network and its shape, as one line of
- * text ("tier=compiled superblocks=.. regs=.. words=.." or
- * "tier=interp reason=.."); compiles the schedule if not cached yet. */
+ * text ("tier=native ..", "tier=compiled superblocks=.. regs=.. words=.." or
+ * "tier=interp reason=.."); compiles the schedule (and the native kernel) if
+ * not cached yet. */
 int mk_net_plan(mk_net *net, const mk_opts *opts, char *out, size_t out_len);
+
+/* Compile everything `opts` will use on `device` now (schedule, native
+ * kernel, device tables) so the first mk_compute_* call does not pay for it.
+ * Replaces nothing in the reference (its /load has no compile step); meant
+ * for the master's /load and for benchmarks. */
+int mk_net_prepare(mk_net *net, const mk_opts *opts, int device);
+
+/* Generated source of the native (tier-3) kernel for `opts` (MK_ELIMIT with
+ * the reason in `out` when the tier is unavailable). */
+int mk_net_jit_source(mk_net *net, const mk_opts *opts, char *out, size_t out_len);
 
 /* Micro-op listing of the compiled schedule for `opts` (MK_ELIMIT if the
  * network is not compilable). */

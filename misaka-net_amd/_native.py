@@ -34,6 +34,9 @@ MK_NODE_MASTER = 2
 
 MK_FLAG_STOP_ON_OUTPUT = 1
 MK_FLAG_FORCE_INTERP = 2
+MK_FLAG_TILE = 4
+MK_FLAG_REFILL = 8
+MK_FLAG_JIT = 16
 
 MK_IN_I64 = 0
 MK_IN_I32 = 1
@@ -107,6 +110,8 @@ SIGNATURES = {
     "mk_net_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "mk_net_plan": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
     "mk_net_sched_disasm": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
+    "mk_net_prepare": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_int]),
+    "mk_net_jit_source": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
     "mk_valu_probe_device": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
     "mk_version": (C.c_char_p, []),
 }

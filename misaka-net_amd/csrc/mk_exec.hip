@@ -24,8 +24,11 @@
 // internal/nodes/stack.go:95-155, internal/nodes/master.go:233-249 and
 // internal/utils/math.go:20-22; see tis_front.cpp for the lowering.
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -35,6 +38,7 @@
 
 #include "../../include/mk.h"
 #include "tis_front.h"
+#include "tis_jit.h"
 #include "tis_sched.h"
 
 namespace mk {
@@ -67,32 +71,10 @@ struct KParams {
     uint64_t lanes;      // resident lanes (grid threads)
 };
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
-{
-    uint64_t z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
 
-__device__ __forceinline__ int32_t gen_value(uint64_t seed, uint32_t kind, uint32_t mask, uint64_t i)
-{
-    const uint64_t h = splitmix64(seed ^ i);
-    if (kind == MK_GEN_MASKED) return (int32_t)((uint32_t)h & mask);
-    if ((i & 15) == 15) {
-        switch ((h >> 32) & 7) {
-        case 0: return INT32_MIN;
-        case 1: return INT32_MIN + 1;
-        case 2: return INT32_MIN + 2;
-        case 3: return -1;
-        case 4: return 0;
-        case 5: return 1;
-        case 6: return INT32_MAX - 1;
-        default: return INT32_MAX;
-        }
-    }
-    return (int32_t)(uint32_t)h;
-}
+#define MK_DEVICE_SRC(...) __VA_ARGS__
+#include "mk_device_common.inc"
+#undef MK_DEVICE_SRC
 
 __device__ __forceinline__ int32_t lane_input(const KParams &p, uint64_t i)
 {
@@ -101,26 +83,6 @@ __device__ __forceinline__ int32_t lane_input(const KParams &p, uint64_t i)
     return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ void write_partials(unsigned long long *partials, uint64_t gid,
-                                               const unsigned long long (&c)[7])
-{
-    unsigned long long v[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) v[k] = wave_sum(c[k]);
-    if ((gid & 63) == 0) {
-        unsigned long long *q = partials + (gid >> 6) * 8;
-#pragma unroll
-        for (int k = 0; k < 7; k++) q[k] = v[k];
-        q[7] = 0;
-    }
-}
 
 // Folds the per-wave partials into the caller's counters: one thread per
 // wave partial, a block tree in LDS, then one atomic per counter per block.
@@ -376,26 +338,6 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
 // micro-op stream (scalar fetch + scalar dispatch, VALU only for the data),
 // and repeats; lanes leave a superblock at BR/JRO/JUMP/END/GUARD/ROUND_END.
 // ------------------------------------------------------------------------
-struct SParams {
-    int in_kind;
-    uint32_t gen_kind;
-    const void *in_data;
-    uint64_t seed;
-    uint64_t offset;
-    uint32_t gen_mask;
-    uint32_t budget;
-    uint64_t n;
-    int32_t *out;
-    uint8_t *status;
-    uint32_t *steps;
-    unsigned long long *partials; // [waves][8] per-wave counters, or null
-    int32_t *slots;      // [nslots][vlanes] stack slots in HBM
-    uint64_t lanes;      // resident threads
-    uint64_t vlanes;     // lanes * K (one input per slot)
-    uint32_t in_off;      // LDS byte offset of the input register (reg * K * B * 8)
-    uint32_t scratch_off; // LDS byte offset of a scratch register (writes of slots outside the group)
-    uint64_t scratch_slot; // HBM slot row for stores of slots outside the group
-};
 
 // `i` must be wave-uniform.  readfirstlane pins the index and every fetched
 // dword to SGPRs: the fetch is scalar loads and the opcode switch a scalar
@@ -421,12 +363,6 @@ __device__ __forceinline__ DOp fetch_dop(const DOp *__restrict__ code, uint32_t 
     return o;
 }
 
-__device__ __forceinline__ int32_t sched_input(const SParams &p, uint64_t i)
-{
-    if (p.in_kind == MK_IN_I64) return (int32_t)((const int64_t *)p.in_data)[i];
-    if (p.in_kind == MK_IN_I32) return ((const int32_t *)p.in_data)[i];
-    return gen_value(p.seed, p.gen_kind, p.gen_mask, p.offset + i);
-}
 
 // ---- tier-2 superblock execution ------------------------------------------
 // LDS register file layout: [reg][slot k][lane] int64, so register r of slot k
@@ -621,8 +557,69 @@ __device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__rest
     }
 }
 
-// Tier-2 kernel: each thread carries K independent inputs ("slots"); one
-// scalar fetch + dispatch of a micro-op serves all K x 64 of them.
+// One waterfall step of a wave: the superblock u of the first active slot of
+// the wave is run for every slot sitting on it ("the group").  A scalar fetch
+// and dispatch of each micro-op serves all K x 64 slots of the group.  fin[k]
+// is set for slots that ended in this step; st/outv are written for them only.
+// Returns false (wave-uniform) once no slot of the wave is active.
+template <int K, int B>
+__device__ __forceinline__ bool sched_step(const DOp *__restrict__ code, const uint32_t *__restrict__ entry,
+                                           const uint32_t *__restrict__ jtab, const SParams &p,
+                                           const Slots<K, B> &S, uint64_t gid, const bool (&act)[K],
+                                           uint32_t (&sb)[K], uint32_t (&steps)[K], bool (&fin)[K],
+                                           uint32_t (&st)[K], int32_t (&outv)[K])
+{
+    bool any = false;
+    uint32_t fsb = 0;
+#pragma unroll
+    for (int k = K - 1; k >= 0; --k) {
+        any = any || act[k];
+        if (act[k]) fsb = sb[k];
+        fin[k] = false;
+    }
+    const unsigned long long anyb = __ballot(any);
+    if (!anyb) return false;
+    const uint32_t u = rfl((uint32_t)__builtin_amdgcn_readlane((int)fsb, __builtin_ctzll(anyb)));
+    bool mine[K], mine_any = false, mine_all = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        mine[k] = act[k] && sb[k] == u;
+        mine_any = mine_any || mine[k];
+        mine_all = mine_all && mine[k];
+    }
+    const bool full = __ballot(mine_any && !mine_all) == 0;
+    if (!mine_any) return true;
+    uint32_t pc = rfl(entry[u]);
+    if (u & 1u) {
+        run_checked<K, B>(code, jtab, pc, p, S, gid, mine, sb, steps, fin, st, outv);
+        return true;
+    }
+    for (;;) {
+        const DOp E = full ? run_data<K, B, true>(code, pc, p, S, gid, mine)
+                           : run_data<K, B, false>(code, pc, p, S, gid, mine);
+        if (E.op == U_GUARD) {
+            // any slot that could reach the budget inside: the whole group
+            // takes the checked variant (exact for every slot)
+            bool need = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) need = need || (mine[k] && (uint64_t)steps[k] + E.inc >= p.budget);
+            if (__ballot(need)) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) sb[k] = mine[k] ? (uint32_t)E.imm : sb[k];
+                return true;
+            }
+            ++pc;
+            continue;
+        }
+        apply_exit<K, B>(E, jtab, S, mine, sb, steps, fin, st, outv);
+        return true;
+    }
+}
+
+
+// Refill scheduling: slot k of thread gid runs inputs gid + k*lanes, then
+// + vlanes, ...; a slot that finishes writes its result and immediately takes
+// its next input (prefetched one input ahead).
 template <int K, int B>
 __global__ void __launch_bounds__(B) tis_sched_exec(const DOp *__restrict__ code, const uint32_t *__restrict__ entry,
                                                     const uint32_t *__restrict__ jtab, SParams p)
@@ -635,9 +632,9 @@ __global__ void __launch_bounds__(B) tis_sched_exec(const DOp *__restrict__ code
 
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0}; // steps, out, done, quiescent, budget, overflow, out-stop
     uint64_t idx[K];
-    bool act[K];
-    uint32_t sb[K], steps[K];
-    int32_t nxt[K];
+    bool act[K], fin[K];
+    uint32_t sb[K], steps[K], st[K];
+    int32_t nxt[K], outv[K];
     int64_t *in_reg = S.at(p.in_off);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -645,85 +642,22 @@ __global__ void __launch_bounds__(B) tis_sched_exec(const DOp *__restrict__ code
         act[k] = idx[k] < p.n;
         sb[k] = 0;
         steps[k] = 0;
+        st[k] = 0;
+        outv[k] = 0;
         nxt[k] = 0;
-        // the next input of each slot is loaded one input ahead, so a refill
-        // never waits on HBM latency
         if (act[k]) {
             in_reg[k * B] = sched_input(p, idx[k]);
             if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
         }
     }
-
-    for (;;) {
-        bool any = false;
-        uint32_t fsb = 0;
-#pragma unroll
-        for (int k = K - 1; k >= 0; --k) {
-            any = any || act[k];
-            if (act[k]) fsb = sb[k];
-        }
-        const unsigned long long anyb = __ballot(any);
-        if (!anyb) break;
-        const uint32_t u = rfl((uint32_t)__builtin_amdgcn_readlane((int)fsb, __builtin_ctzll(anyb)));
-        bool mine[K], mine_any = false, mine_all = true;
+    while (sched_step<K, B>(code, entry, jtab, p, S, gid, act, sb, steps, fin, st, outv)) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            mine[k] = act[k] && sb[k] == u;
-            mine_any = mine_any || mine[k];
-            mine_all = mine_all && mine[k];
-        }
-        const bool full = __ballot(mine_any && !mine_all) == 0;
-        if (!mine_any) continue;
-        uint32_t pc = rfl(entry[u]);
-        bool done[K];
-        uint32_t st[K];
-        int32_t outv[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            done[k] = false;
-            st[k] = 0;
-            outv[k] = 0;
-        }
-        if (u & 1u) {
-            run_checked<K, B>(code, jtab, pc, p, S, gid, mine, sb, steps, done, st, outv);
-        } else {
-            for (;;) {
-                const DOp E = full ? run_data<K, B, true>(code, pc, p, S, gid, mine)
-                                   : run_data<K, B, false>(code, pc, p, S, gid, mine);
-                if (E.op == U_GUARD) {
-                    // any slot that could reach the budget inside: the whole
-                    // group takes the checked variant (exact for every slot)
-                    bool need = false;
-#pragma unroll
-                    for (int k = 0; k < K; ++k) need = need || (mine[k] && (uint64_t)steps[k] + E.inc >= p.budget);
-                    if (__ballot(need)) {
-#pragma unroll
-                        for (int k = 0; k < K; ++k)
-                            if (mine[k]) sb[k] = (uint32_t)E.imm;
-                        break;
-                    }
-                    ++pc;
-                    continue;
-                }
-                apply_exit<K, B>(E, jtab, S, mine, sb, steps, done, st, outv);
-                break;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!done[k]) continue;
-            const uint32_t reason = st[k] & MK_ST_REASON_MASK;
-            const bool has = (st[k] & MK_ST_HAS_OUTPUT) != 0;
-            p.out[idx[k]] = has ? outv[k] : 0;
+            if (!fin[k]) continue;
+            p.out[idx[k]] = (st[k] & MK_ST_HAS_OUTPUT) ? outv[k] : 0;
             p.status[idx[k]] = (uint8_t)st[k];
             if (p.steps) p.steps[idx[k]] = steps[k];
-            cnt[0] += steps[k];
-            cnt[1] += has;
-            cnt[2] += 1;
-            cnt[3] += reason == MK_ST_QUIESCENT;
-            cnt[4] += reason == MK_ST_BUDGET;
-            cnt[5] += reason == MK_ST_STACK_OVERFLOW;
-            cnt[6] += reason == MK_ST_OUTPUT_STOP;
+            count_lane(cnt, steps[k], st[k]);
             idx[k] += stride;
             act[k] = idx[k] < p.n;
             sb[k] = 0;
@@ -733,6 +667,99 @@ __global__ void __launch_bounds__(B) tis_sched_exec(const DOp *__restrict__ code
                 if (idx[k] + stride < p.n) nxt[k] = sched_input(p, idx[k] + stride);
             }
         }
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+
+// K contiguous inputs at `base` (ragged tail: only those < n).
+template <int K>
+__device__ __forceinline__ void tile_inputs(const SParams &p, uint64_t base, int32_t (&v)[K])
+{
+    if (p.io_vec && base + K <= p.n) {
+        const int32_t *src = (const int32_t *)p.in_data + base;
+        if constexpr (K == 4) {
+            const int4 q = *reinterpret_cast<const int4 *>(src);
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else if constexpr (K == 2) {
+            const int2 q = *reinterpret_cast<const int2 *>(src);
+            v[0] = q.x, v[1] = q.y;
+        } else {
+            v[0] = src[0];
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = base + k < p.n ? sched_input(p, base + k) : 0;
+}
+
+// Tile scheduling: a block takes tiles of K*B contiguous inputs (grid-stride),
+// thread tid owns inputs base = tile*K*B + tid*K .. base+K-1, the next tile's
+// inputs are loaded while this one runs, and results leave in vector stores
+// once every lane of the tile has finished.
+template <int K, int B>
+__global__ void __launch_bounds__(B) tis_sched_tile(const DOp *__restrict__ code, const uint32_t *__restrict__ entry,
+                                                    const uint32_t *__restrict__ jtab, SParams p)
+{
+    extern __shared__ int64_t R[]; // [nregs][K][B]
+    const uint32_t tid = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
+    const Slots<K, B> S{reinterpret_cast<char *>(R) + tid * 8};
+    const uint64_t tile = (uint64_t)K * B, ntiles = (p.n + tile - 1) / tile;
+
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    int64_t *in_reg = S.at(p.in_off);
+    int32_t nxt[K];
+    uint64_t t = blockIdx.x;
+    if (t < ntiles) tile_inputs<K>(p, t * tile + (uint64_t)tid * K, nxt);
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * tile + (uint64_t)tid * K;
+        bool act[K], fin[K];
+        uint32_t sb[K], steps[K], st[K];
+        int32_t outv[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            act[k] = base + k < p.n;
+            sb[k] = 0;
+            steps[k] = 0;
+            st[k] = 0;
+            outv[k] = 0;
+            in_reg[k * B] = nxt[k];
+        }
+        if (t + gridDim.x < ntiles) tile_inputs<K>(p, base + (uint64_t)gridDim.x * tile, nxt);
+        while (sched_step<K, B>(code, entry, jtab, p, S, gid, act, sb, steps, fin, st, outv)) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) act[k] = act[k] && !fin[k];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) outv[k] = (st[k] & MK_ST_HAS_OUTPUT) ? outv[k] : 0;
+        if (p.io_vec && base + K <= p.n) {
+            if constexpr (K == 4) {
+                *reinterpret_cast<int4 *>(p.out + base) = make_int4(outv[0], outv[1], outv[2], outv[3]);
+                *reinterpret_cast<uint32_t *>(p.status + base) =
+                    (st[0] & 0xffu) | (st[1] & 0xffu) << 8 | (st[2] & 0xffu) << 16 | st[3] << 24;
+                if (p.steps)
+                    *reinterpret_cast<uint4 *>(p.steps + base) = make_uint4(steps[0], steps[1], steps[2], steps[3]);
+            } else if constexpr (K == 2) {
+                *reinterpret_cast<int2 *>(p.out + base) = make_int2(outv[0], outv[1]);
+                *reinterpret_cast<uint16_t *>(p.status + base) = (uint16_t)((st[0] & 0xffu) | (st[1] & 0xffu) << 8);
+                if (p.steps) *reinterpret_cast<uint2 *>(p.steps + base) = make_uint2(steps[0], steps[1]);
+            } else {
+                p.out[base] = outv[0];
+                p.status[base] = (uint8_t)st[0];
+                if (p.steps) p.steps[base] = steps[0];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (base + k >= p.n) continue;
+                p.out[base + k] = outv[k];
+                p.status[base + k] = (uint8_t)st[k];
+                if (p.steps) p.steps[base + k] = steps[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (base + k < p.n) count_lane(cnt, steps[k], st[k]);
     }
     if (p.partials) write_partials(p.partials, gid, cnt);
 }
@@ -781,14 +808,32 @@ struct SchedDev {
     size_t slots_bytes = 0;
 };
 
+// Tier 3: the schedule compiled to a native kernel (tis_jit.h).
+struct JitDev {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    int per_cu = 0;
+};
+
+struct JitState {
+    bool tried = false, ok = false;
+    std::string why;          // reason the native tier is unavailable
+    std::vector<char> code;   // gfx950 code object
+    double compile_s = 0;
+    size_t src_bytes = 0;
+    JitDev dev[kMaxDevices];
+};
+
 // A compiled schedule for one (stack_cap, stop_on_output) pair.
 struct SchedCache {
     uint32_t cap = 0;
     bool soo = false;
     bool ok = false;
+    bool tile = false; // default lane scheduling (sched_default_tile)
     std::string why;
     SchedProgram prog;
     SchedDev dev[kMaxDevices];
+    JitState jit;
 };
 
 struct DevCtx {
@@ -829,6 +874,7 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_entry);
                 (void)hipFree(sc->dev[d].d_jtab);
                 (void)hipFree(sc->dev[d].d_slots);
+                if (sc->jit.dev[d].mod) (void)hipModuleUnload(sc->jit.dev[d].mod);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
         }
@@ -929,6 +975,12 @@ void resolve_opts(const mk_opts *o, uint32_t &budget, uint32_t &cap, uint32_t &f
     flags = o ? o->flags : 0u;
 }
 
+// Default lane scheduling: tiles.  Measured on MI355X (profiles/r01_modes.txt)
+// tiles beat refill on every configuration, including the variable-length
+// C5 countdown (vector I/O and one shared superblock walk per tile outweigh
+// the idle slots of finished lanes).
+bool sched_default_tile(const SchedProgram &) { return true; }
+
 // Caller holds h->mu.  Compiles the schedule for (cap, soo) once.
 SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
 {
@@ -939,6 +991,7 @@ SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
     sc->soo = soo;
     SchedLimits lim;
     sc->ok = compile_schedule(h->net, cap, soo, lim, sc->prog, sc->why);
+    sc->tile = sc->ok && sched_default_tile(sc->prog);
     h->sched.push_back(std::move(sc));
     return h->sched.back().get();
 }
@@ -954,15 +1007,22 @@ void sched_geometry(uint32_t nregs, uint32_t &B, uint32_t &K)
     while (K > 1 && r * K * B * 8 > 40 * 1024) K >>= 1;
 }
 
-void *sched_kernel(int K, int B)
+template <int K, int B>
+void *sched_kernel_t(bool tile)
 {
-    if (B == 256 && K == 4) return reinterpret_cast<void *>(&tis_sched_exec<4, 256>);
-    if (B == 256 && K == 2) return reinterpret_cast<void *>(&tis_sched_exec<2, 256>);
-    if (B == 256 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 256>);
-    if (B == 128 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 128>);
-    if (B == 64 && K == 1) return reinterpret_cast<void *>(&tis_sched_exec<1, 64>);
+    return tile ? reinterpret_cast<void *>(&tis_sched_tile<K, B>) : reinterpret_cast<void *>(&tis_sched_exec<K, B>);
+}
+
+void *sched_kernel(int K, int B, bool tile)
+{
+    if (B == 256 && K == 4) return sched_kernel_t<4, 256>(tile);
+    if (B == 256 && K == 2) return sched_kernel_t<2, 256>(tile);
+    if (B == 256 && K == 1) return sched_kernel_t<1, 256>(tile);
+    if (B == 128 && K == 1) return sched_kernel_t<1, 128>(tile);
+    if (B == 64 && K == 1) return sched_kernel_t<1, 64>(tile);
     return nullptr;
 }
+
 
 // Caller holds h->mu.
 int ensure_sched_device(SchedCache *sc, int d)
@@ -1011,7 +1071,8 @@ int launch_stats_reduce(DevCtx &c, uint64_t lanes, uint64_t *d_stats, hipStream_
 
 // Caller holds h->mu.  Tier-2 launch; asynchronous on `stream`.
 int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
-                        uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, hipStream_t stream)
+                        uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, uint32_t flags,
+                        hipStream_t stream)
 {
     int rc = ensure_sched_device(sc, d);
     if (rc) return rc;
@@ -1024,11 +1085,12 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     const int B = (int)sd.block, K = (int)sd.slots;
     const size_t lds = (size_t)(P.nregs + 1) * K * B * 8; // + one scratch register
     if (lds > 160 * 1024) return MK_ELIMIT;
-    void *fn = sched_kernel(K, B);
+    const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
+    void *fn = sched_kernel(K, B, tile);
     if (!fn) return MK_ELIMIT;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    const uint64_t want = (n + (uint64_t)B * K - 1) / ((uint64_t)B * K);
+    const uint64_t want = (n + (uint64_t)B * K - 1) / ((uint64_t)B * K); // tiles
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(c.cus, 1);
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
     const uint64_t lanes = (uint64_t)blocks * B;
@@ -1066,11 +1128,149 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     p.in_off = P.in_reg * (uint32_t)(K * B * 8);
     p.scratch_off = P.nregs * (uint32_t)(K * B * 8);
     p.scratch_slot = P.nslots;
+    const uintptr_t va = 4u * (uintptr_t)K; // K x int32 vector
+    p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
+               (uintptr_t)d_status % (uintptr_t)K == 0 && (uintptr_t)d_steps % va == 0;
     const DOp *code = sd.d_code;
     const uint32_t *entry = sd.d_entry, *jtab = sd.d_jtab;
     void *args[] = {(void *)&code, (void *)&entry, (void *)&jtab, (void *)&p};
     if (hipLaunchKernel(fn, dim3(blocks), dim3(B), args, lds, stream) != hipSuccess) return MK_EDEVICE;
     return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
+}
+
+// ---- tier 3: native kernel per schedule (tis_jit.h) ------------------------
+// Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
+// gfx950); the code object is loaded per device on first use.  MK_JIT=0 in
+// the environment disables the tier.
+bool jit_compile(SchedCache *sc)
+{
+    JitState &J = sc->jit;
+    if (J.tried) return J.ok;
+    J.tried = true;
+    if (!sc->ok) {
+        J.why = "no compiled schedule (" + sc->why + ")";
+        return false;
+    }
+    const char *env = std::getenv("MK_JIT");
+    if (env && std::strcmp(env, "0") == 0) {
+        J.why = "disabled by MK_JIT=0";
+        return false;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string lane;
+    if (!jit_lane_source(sc->prog, JitLimits{}, lane, J.why)) return false;
+    const std::string src = jit_module_source(lane);
+    J.src_bytes = src.size();
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        J.why = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        (void)hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
+        J.why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
+        (void)hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t cs = 0;
+    if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+        J.why = "hiprtc produced no code";
+        (void)hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    J.code.resize(cs);
+    (void)hiprtcGetCode(prog, J.code.data());
+    (void)hiprtcDestroyProgram(&prog);
+    J.compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    J.ok = true;
+    return true;
+}
+
+// Caller holds h->mu.
+int ensure_jit_device(SchedCache *sc, int d)
+{
+    JitDev &jd = sc->jit.dev[d];
+    if (jd.fn) return MK_OK;
+    DeviceGuard g(d);
+    if (hipModuleLoadData(&jd.mod, sc->jit.code.data()) != hipSuccess) return MK_EDEVICE;
+    if (hipModuleGetFunction(&jd.fn, jd.mod, kJitKernel) != hipSuccess) return MK_EDEVICE;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, kJitBlock, 0) != hipSuccess ||
+        jd.per_cu < 1)
+        jd.per_cu = 1;
+    return MK_OK;
+}
+
+// Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
+int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
+                      uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, hipStream_t stream)
+{
+    int rc = ensure_jit_device(sc, d);
+    if (rc) return rc;
+    DevCtx &c = h->dev[d];
+    SchedDev &sd = sc->dev[d];
+    JitDev &jd = sc->jit.dev[d];
+    const SchedProgram &P = sc->prog;
+    DeviceGuard g(d);
+    const uint64_t want = (n + kJitBlock - 1) / kJitBlock;
+    const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    const uint64_t lanes = (uint64_t)blocks * kJitBlock;
+    if (P.nslots) {
+        const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
+        if (need > sd.slots_bytes) {
+            if (sd.d_slots) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(sd.d_slots);
+                sd.d_slots = nullptr;
+                sd.slots_bytes = 0;
+            }
+            if (hipMalloc(&sd.d_slots, need) != hipSuccess) return MK_ENOMEM;
+            sd.slots_bytes = need;
+        }
+    }
+    SParams p{};
+    p.in_kind = in->kind;
+    p.gen_kind = in->gen_kind;
+    p.in_data = in->data;
+    p.seed = in->seed;
+    p.offset = in->offset;
+    p.gen_mask = in->gen_mask;
+    p.budget = budget;
+    p.n = n;
+    p.out = d_out;
+    p.status = d_status;
+    p.steps = d_steps;
+    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = d_stats ? c.d_partials : nullptr;
+    p.slots = P.nslots ? sd.d_slots : nullptr;
+    p.lanes = lanes;
+    p.vlanes = lanes;
+    void *args[] = {(void *)&p};
+    if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, kJitBlock, 1, 1, 0, stream, args, nullptr) != hipSuccess)
+        return MK_EDEVICE;
+    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
+}
+
+enum Tier { TIER_NONE, TIER_INTERP, TIER_COMPILED, TIER_NATIVE };
+
+// Caller holds h->mu.  The tier a launch with `flags` runs on: tier 1 when
+// forced; else the native kernel unless tier 2 was asked for (TILE/REFILL);
+// else the superblock interpreter; tier 1 when the schedule compiler gave up.
+Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, SchedCache **out)
+{
+    *out = nullptr;
+    if (flags & MK_FLAG_FORCE_INTERP) return TIER_INTERP;
+    SchedCache *sc = get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
+    *out = sc;
+    const bool want_jit = (flags & MK_FLAG_JIT) || !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL));
+    if (want_jit && jit_compile(sc)) return TIER_NATIVE;
+    if (flags & MK_FLAG_JIT) return TIER_NONE;
+    return sc->ok ? TIER_COMPILED : TIER_INTERP;
 }
 
 // Caller holds h->mu.  Asynchronous on `stream`.
@@ -1084,9 +1284,13 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     DeviceGuard g(d);
     uint32_t budget, cap, flags;
     resolve_opts(o, budget, cap, flags);
-    if (!(flags & MK_FLAG_FORCE_INTERP)) {
-        SchedCache *sc = get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
-        if (sc->ok) return launch_sched_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, stream);
+    SchedCache *sc = nullptr;
+    switch (pick_tier(h, cap, flags, &sc)) {
+    case TIER_NATIVE: return launch_jit_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, stream);
+    case TIER_COMPILED:
+        return launch_sched_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, flags, stream);
+    case TIER_NONE: return MK_ELIMIT; // native tier demanded but unavailable (mk_net_plan says why)
+    default: break;
     }
     Launch L;
     if ((rc = plan_launch(h->net, c, n, cap, L))) return rc;
@@ -1335,20 +1539,68 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (!h) return MK_EINVAL;
     uint32_t budget, cap, flags;
     mk::resolve_opts(opts, budget, cap, flags);
-    char buf[512];
-    if (flags & MK_FLAG_FORCE_INTERP) {
-        snprintf(buf, sizeof buf, "tier=interp reason=forced");
+    char buf[1024];
+    std::lock_guard<std::mutex> lk(h->mu);
+    mk::SchedCache *sc = nullptr;
+    const mk::Tier t = mk::pick_tier(h, cap, flags, &sc);
+    if (t == mk::TIER_INTERP) {
+        snprintf(buf, sizeof buf, "tier=interp reason=%s", sc ? sc->why.c_str() : "forced");
         return mk::copy_out(out, out_len, buf);
     }
+    if (t == mk::TIER_NONE) {
+        snprintf(buf, sizeof buf, "tier=none reason=native tier unavailable: %s", sc->jit.why.c_str());
+        (void)mk::copy_out(out, out_len, buf);
+        return MK_ELIMIT;
+    }
+    const mk::SchedProgram &P = sc->prog;
+    int len = snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu rounds=%llu", P.nsb,
+                       P.nregs, P.nslots, P.code.size(), P.jtab.size(), (unsigned long long)P.sym_rounds);
+    std::string s;
+    if (t == mk::TIER_NATIVE) {
+        char tail[160];
+        snprintf(tail, sizeof tail, " source=%zuB code=%zuB compile=%.2fs", sc->jit.src_bytes, sc->jit.code.size(),
+                 sc->jit.compile_s);
+        s = std::string("tier=native ") + buf + tail;
+    } else {
+        const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
+        uint32_t B, K;
+        mk::sched_geometry(P.nregs, B, K);
+        snprintf(buf + len, sizeof buf - len, " lanes=%s K=%u B=%u native=%s", tile ? "tile" : "refill", K, B,
+                 sc->jit.tried ? (sc->jit.ok ? "ok" : sc->jit.why.c_str()) : "not-requested");
+        s = std::string("tier=compiled ") + buf;
+    }
+    return mk::copy_out(out, out_len, s);
+}
+
+int mk_net_prepare(mk_net *h, const mk_opts *opts, int device)
+{
+    if (!h || device < 0 || device >= mk::kMaxDevices) return MK_EINVAL;
+    uint32_t budget, cap, flags;
+    mk::resolve_opts(opts, budget, cap, flags);
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = mk::ensure_device(h, device);
+    if (rc) return rc;
+    mk::SchedCache *sc = nullptr;
+    switch (mk::pick_tier(h, cap, flags, &sc)) {
+    case mk::TIER_NATIVE: return mk::ensure_jit_device(sc, device);
+    case mk::TIER_COMPILED: return mk::ensure_sched_device(sc, device);
+    case mk::TIER_NONE: return MK_ELIMIT;
+    default: return MK_OK;
+    }
+}
+
+int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
+{
+    if (!h) return MK_EINVAL;
+    uint32_t budget, cap, flags;
+    mk::resolve_opts(opts, budget, cap, flags);
     std::lock_guard<std::mutex> lk(h->mu);
     mk::SchedCache *sc = mk::get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
-    if (sc->ok)
-        snprintf(buf, sizeof buf, "tier=compiled superblocks=%u regs=%u slots=%u words=%zu jtab=%zu rounds=%llu",
-                 sc->prog.nsb, sc->prog.nregs, sc->prog.nslots, sc->prog.code.size(), sc->prog.jtab.size(),
-                 (unsigned long long)sc->prog.sym_rounds);
-    else
-        snprintf(buf, sizeof buf, "tier=interp reason=%s", sc->why.c_str());
-    return mk::copy_out(out, out_len, buf);
+    std::string lane, why;
+    if (!sc->ok) why = sc->why;
+    else if (mk::jit_lane_source(sc->prog, mk::JitLimits{}, lane, why)) return mk::copy_out(out, out_len, mk::jit_module_source(lane));
+    (void)mk::copy_out(out, out_len, why);
+    return MK_ELIMIT;
 }
 
 int mk_net_sched_disasm(mk_net *h, const mk_opts *opts, char *out, size_t out_len)

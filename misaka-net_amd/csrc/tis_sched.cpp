@@ -595,7 +595,7 @@ void Compiler::exit_branch(int n, uint8_t cond, uint16_t target)
     const uint32_t len = net_.len[n];
     Ctl t = ctl_, f = ctl_;
     t.ip[n] = target;
-    f.ip[n] = (uint16_t)((ctl_.ip[n] + 1 == len) ? 0 : ctl_.ip[n] + 1);
+    f.ip[n] = (uint16_t)(((uint32_t)ctl_.ip[n] + 1 == len) ? 0 : ctl_.ip[n] + 1);
     t.changed = f.changed = true;
     t.pos = f.pos = (uint8_t)(n + 1);
     steps_++;
@@ -678,7 +678,7 @@ int Compiler::attempt(int n)
     uint16_t &ip = ctl_.ip[n];
     const Insn &I = net_.code[net_.base[n] + ip];
     auto retire = [&]() {
-        ip = (uint16_t)((ip + 1 == len) ? 0 : ip + 1);
+        ip = (uint16_t)(((uint32_t)ip + 1 == len) ? 0 : ip + 1);
         steps_++;
         ctl_.changed = true;
     };

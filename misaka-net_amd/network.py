@@ -65,13 +65,23 @@ class BatchResult:
         return self.status & N.MK_ST_REASON_MASK
 
 
+_MODES = {None: 0, "interp": N.MK_FLAG_FORCE_INTERP, "tile": N.MK_FLAG_TILE, "refill": N.MK_FLAG_REFILL,
+          "jit": N.MK_FLAG_JIT}
+
+
 def make_opts(budget=None, stack_cap=None, stop_on_output=False, devices: Optional[Iterable[int]] = None,
-              interp=False):
-    """mk_opts; ``interp=True`` forces the direct bytecode interpreter (tier 1)."""
+              interp=False, mode=None):
+    """mk_opts.  ``mode``: None (automatic), "jit" (demand the native
+    per-network kernel, tier 3), "tile" or "refill" (the tier-2 superblock
+    interpreter with that lane scheduling, see mk.h MK_FLAG_TILE), "interp"
+    (the direct bytecode interpreter, tier 1; same as ``interp=True``)."""
+    if mode not in _MODES:
+        raise ValueError(f"unknown executor mode {mode!r}")
     o = N.mk_opts()
     o.budget = int(budget or 0)
     o.stack_cap = int(stack_cap or 0)
-    o.flags = (N.MK_FLAG_STOP_ON_OUTPUT if stop_on_output else 0) | (N.MK_FLAG_FORCE_INTERP if interp else 0)
+    o.flags = ((N.MK_FLAG_STOP_ON_OUTPUT if stop_on_output else 0) | (N.MK_FLAG_FORCE_INTERP if interp else 0)
+               | _MODES[mode])
     mask = 0
     for d in devices or ():
         mask |= 1 << int(d)
@@ -139,11 +149,29 @@ class Network:
         N.check(N.lib().mk_net_disasm(self._h, buf, len(buf)))
         return buf.value.decode()
 
-    def plan(self, *, stack_cap=None, stop_on_output=False, interp=False) -> str:
-        """Which executor tier runs this network (compiles the schedule once)."""
-        buf = C.create_string_buffer(1024)
-        o = make_opts(None, stack_cap, stop_on_output, None, interp)
-        N.check(N.lib().mk_net_plan(self._h, C.byref(o), buf, len(buf)))
+    def plan(self, *, stack_cap=None, stop_on_output=False, interp=False, mode=None) -> str:
+        """Which executor tier runs this network (compiles the schedule, and
+        the native kernel, once)."""
+        buf = C.create_string_buffer(4096)
+        o = make_opts(None, stack_cap, stop_on_output, None, interp, mode)
+        rc = N.lib().mk_net_plan(self._h, C.byref(o), buf, len(buf))
+        if rc == N.MK_ELIMIT:
+            return buf.value.decode()
+        N.check(rc)
+        return buf.value.decode()
+
+    def prepare(self, *, stack_cap=None, stop_on_output=False, mode=None, device=0):
+        """Compile everything a launch with these options uses on ``device``."""
+        o = make_opts(None, stack_cap, stop_on_output, None, False, mode)
+        N.check(N.lib().mk_net_prepare(self._h, C.byref(o), device), self.plan(stack_cap=stack_cap,
+                                                                             stop_on_output=stop_on_output, mode=mode))
+
+    def jit_source(self, *, stack_cap=None, stop_on_output=False) -> str:
+        """hiprtc source of the native (tier-3) kernel."""
+        buf = C.create_string_buffer(1 << 24)
+        o = make_opts(None, stack_cap, stop_on_output)
+        rc = N.lib().mk_net_jit_source(self._h, C.byref(o), buf, len(buf))
+        N.check(rc, buf.value.decode())
         return buf.value.decode()
 
     def sched_disasm(self, *, stack_cap=None, stop_on_output=False) -> str:
@@ -153,7 +181,7 @@ class Network:
         return buf.value.decode()
 
     def compute_batch(self, values, *, budget=None, stack_cap=None, stop_on_output=False, devices=None, steps=True,
-                      interp=False):
+                      interp=False, mode=None):
         """Evaluate independent /compute inputs (strconv.Atoi int64 values,
         truncated to int32 at GetInput like master.go:237) on the GPU(s)."""
         v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
@@ -161,7 +189,7 @@ class Network:
         out = np.zeros(n, np.int32)
         st = np.zeros(n, np.uint8)
         sp = np.zeros(n, np.uint32) if steps else None
-        o = make_opts(budget, stack_cap, stop_on_output, devices, interp)
+        o = make_opts(budget, stack_cap, stop_on_output, devices, interp, mode)
         rc = N.lib().mk_compute_batch(
             self._h,
             v.ctypes.data_as(C.c_void_p),
@@ -176,7 +204,7 @@ class Network:
 
     def compute_device(self, n, *, out_ptr, status_ptr, steps_ptr=None, stats_ptr=None, device=0, stream=None,
                        in_ptr=None, in_kind=N.MK_IN_I32, seed=0, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0,
-                       budget=None, stack_cap=None, stop_on_output=False, interp=False):
+                       budget=None, stack_cap=None, stop_on_output=False, interp=False, mode=None):
         """Launch on device memory (raw pointers, e.g. torch ``data_ptr()``);
         asynchronous on ``stream`` (a HIP stream handle, e.g.
         ``torch.cuda.current_stream().cuda_stream``)."""
@@ -187,7 +215,7 @@ class Network:
         mi.gen_kind = gen_kind
         mi.gen_mask = gen_mask
         mi.offset = offset
-        o = make_opts(budget, stack_cap, stop_on_output, None, interp)
+        o = make_opts(budget, stack_cap, stop_on_output, None, interp, mode)
         rc = N.lib().mk_compute_device(
             self._h, device, C.byref(mi), n, out_ptr, status_ptr, steps_ptr, stats_ptr, C.byref(o), stream
         )

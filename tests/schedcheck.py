@@ -25,6 +25,7 @@ def lib():
         h.mkc_free.argtypes = [C.c_void_p]
         h.mkc_emulate.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        h.mkc_jit_lane.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_char_p, C.c_size_t]
         _lib = h
     return _lib
 
@@ -33,7 +34,7 @@ class NotCompiled(Exception):
     pass
 
 
-def emulate(nodes, xs, *, budget=None, stack_cap=None, stop_on_output=False, want_plan=False):
+def _load(nodes):
     rows = [(n.name, n.kind, n.program) if hasattr(n, "name") else tuple(n) for n in nodes]
     kinds = {"program": 0, "stack": 1, "master": 2}
     arr = (N.mk_node_desc * len(rows))()
@@ -45,6 +46,27 @@ def emulate(nodes, xs, *, budget=None, stack_cap=None, stop_on_output=False, wan
     err = C.create_string_buffer(4096)
     h = lib().mkc_load(arr, len(rows), err, len(err))
     assert h, err.value
+    return h, keep
+
+
+def jit_lane(nodes, *, stack_cap=None, stop_on_output=False):
+    """(source of the native tier's lane function, stack slots per lane)."""
+    h, _keep = _load(nodes)
+    try:
+        ns = C.c_uint32()
+        buf = C.create_string_buffer(1 << 24)
+        rc = lib().mkc_jit_lane(h, 1024 if stack_cap is None else stack_cap, 1 if stop_on_output else 0,
+                                C.byref(ns), buf, len(buf))
+        if rc == 1:
+            raise NotCompiled(buf.value.decode())
+        assert rc == 0, rc
+        return buf.value.decode(), ns.value
+    finally:
+        lib().mkc_free(h)
+
+
+def emulate(nodes, xs, *, budget=None, stack_cap=None, stop_on_output=False, want_plan=False):
+    h, _keep = _load(nodes)
     try:
         v = np.ascontiguousarray(np.asarray(xs, dtype=np.int64))
         out = np.zeros(v.size, np.int32)

@@ -18,6 +18,10 @@ SEED = 0x4D49534B41
 THREADS = min(16, os.cpu_count() or 1)
 
 
+def _m(mode):
+    return None if mode == "auto" else mode
+
+
 def oracle(nodes, xs, **kw):
     return po.OracleNet(nodes).compute_batch(xs, threads=THREADS, **kw)
 
@@ -40,10 +44,13 @@ def test_readme_kat_on_gpu(gpu):
     assert (r.status == 0x11).all() and (r.steps == 12).all()
 
 
-TIERS = [pytest.param(False, id="compiled"), pytest.param(True, id="interp")]
+# "auto": the default path (the native per-network kernel when the schedule
+# fits its limits, else tier 2); tier 2 with both lane schedulings; tier 1
+MODES = ["auto", "tile", "refill", "interp"]
+NATIVE = {"c2_example", "c3_sample", "c5_countdown"}  # configs whose default path is the native tier
 
 
-@pytest.mark.parametrize("interp", TIERS)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize(
     "name,nodes,n,gen",
     [
@@ -53,57 +60,67 @@ TIERS = [pytest.param(False, id="compiled"), pytest.param(True, id="interp")]
         ("c5_countdown", mk.networks.countdown_network(), 1 << 15, (N.MK_GEN_MASKED, 1023)),
     ],
 )
-def test_configs_bit_exact(gpu, name, nodes, n, gen, interp):
+def test_configs_bit_exact(gpu, name, nodes, n, gen, mode):
     xs = po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1])
     net = mk.Network(nodes)
-    if not interp:
-        assert net.plan().startswith("tier=compiled"), net.plan()
-    got = net.compute_batch(xs, interp=interp)
+    mode = None if mode == "auto" else mode
+    plan = net.plan(mode=mode)
+    if mode is None:
+        assert plan.startswith("tier=native" if name in NATIVE else "tier=compiled"), plan
+    elif mode != "interp":
+        assert plan.startswith("tier=compiled"), plan
+    got = net.compute_batch(xs, mode=mode)
     assert_same(got, oracle(nodes, xs), name)
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_c4_deep_stacks_spill_to_hbm(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_c4_deep_stacks_spill_to_hbm(gpu, mode):
     nodes = mk.networks.pipeline_network(1024)
     xs = po.gen_inputs(SEED, 600)
-    got = mk.Network(nodes).compute_batch(xs, interp=interp)
+    got = mk.Network(nodes).compute_batch(xs, mode=_m(mode))
     ref = oracle(nodes, xs)
     assert_same(got, ref, "c4 D=1024")
     assert (got.status == 0x11).all()
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_c5_zero_trip_and_maximum_trip(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_c5_zero_trip_and_maximum_trip(gpu, mode):
     nodes = mk.networks.countdown_network()
     xs = np.arange(0, 1024, dtype=np.int64)
-    assert_same(mk.Network(nodes).compute_batch(xs, interp=interp), oracle(nodes, xs), "c5 all trip counts")
+    assert_same(mk.Network(nodes).compute_batch(xs, mode=_m(mode)), oracle(nodes, xs), "c5 all trip counts")
 
 
-@pytest.mark.parametrize("interp", TIERS)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", range(0, 240, 1))
-def test_random_networks_bit_exact(gpu, seed, interp):
+def test_random_networks_bit_exact(gpu, seed, mode):
     rows = random_network(seed)
     xs = po.gen_inputs(seed * 7919 + 1, 256)
     cap = [1, 3, 8, 16, 17, 40, 1024][seed % 7]
     kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=cap, stop_on_output=(seed % 5 == 4))
-    got = mk.Network(rows).compute_batch(xs, interp=interp, **kw)
+    net = mk.Network(rows)
+    got = net.compute_batch(xs, mode=_m(mode), **kw)
+    if mode == "auto":  # the default path really is the native tier for these small networks
+        plan = net.plan(stack_cap=kw["stack_cap"], stop_on_output=kw["stop_on_output"])
+        assert plan.startswith(("tier=native", "tier=interp")), plan
     assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_budget_and_stop_on_output(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_budget_and_stop_on_output(gpu, mode):
     nodes = [("a", "program", "JRO 0"), ("b", "program", "OUT 3\nJRO 0")]
-    got = mk.Network(nodes).compute_batch([0] * 70, budget=11, interp=interp)
+    got = mk.Network(nodes).compute_batch([0] * 70, budget=11, mode=_m(mode))
     assert (got.steps == 12).all() and (got.status == (N.MK_ST_BUDGET | N.MK_ST_HAS_OUTPUT)).all()
-    got = mk.Network(nodes).compute_batch([0] * 70, stop_on_output=True, interp=interp)
+    got = mk.Network(nodes).compute_batch([0] * 70, stop_on_output=True, mode=_m(mode))
     assert (got.steps == 2).all() and (got.status == (N.MK_ST_OUTPUT_STOP | N.MK_ST_HAS_OUTPUT)).all()
 
 
+@pytest.mark.parametrize("mode", ["auto", "tile", "refill"])
 @pytest.mark.parametrize("budget", [1, 11, 12, 13, 5000])
-def test_compiled_budget_boundaries(gpu, budget):
+def test_compiled_budget_boundaries(gpu, budget, mode):
     for nodes, kind in ((mk.networks.example_network(), 0), (mk.networks.countdown_network(), 1)):
         xs = po.gen_inputs(SEED, 3000, kind=kind, mask=1023)
-        assert_same(mk.Network(nodes).compute_batch(xs, budget=budget), oracle(nodes, xs, budget=budget), str(budget))
+        got = mk.Network(nodes).compute_batch(xs, budget=budget, mode=_m(mode))
+        assert_same(got, oracle(nodes, xs, budget=budget), str(budget))
 
 
 def test_empty_batch(gpu):
@@ -111,12 +128,13 @@ def test_empty_batch(gpu):
     assert got.out.size == 0
 
 
-def test_ragged_sizes(gpu):
+@pytest.mark.parametrize("mode", MODES)
+def test_ragged_sizes(gpu, mode):
     nodes = mk.networks.sample_network()
     net = mk.Network(nodes)
-    for n in [1, 63, 64, 65, 255, 257, 1000, 4097]:
+    for n in [1, 2, 3, 5, 63, 64, 65, 255, 257, 1000, 1023, 1025, 4097]:
         xs = po.gen_inputs(n, n)
-        assert_same(net.compute_batch(xs), oracle(nodes, xs), f"n={n}")
+        assert_same(net.compute_batch(xs, mode=_m(mode)), oracle(nodes, xs), f"n={n}")
 
 
 def test_concurrent_host_calls(gpu):
@@ -146,7 +164,7 @@ def test_device_generator_matches_oracle(gpu):
     assert np.array_equal(d.cpu().numpy(), po.gen_inputs(SEED, n, offset=12345).astype(np.int32))
 
 
-def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FULL, 0), offset=0, interp=False):
+def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FULL, 0), offset=0, mode=None):
     import torch
 
     out = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -156,31 +174,37 @@ def _device_run(net, n, *, in_tensor=None, in_kind=N.MK_IN_I32, gen=(N.MK_GEN_FU
     net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), steps_ptr=sp.data_ptr(),
                        stats_ptr=stats.data_ptr(), in_ptr=None if in_tensor is None else in_tensor.data_ptr(),
                        in_kind=in_kind, seed=SEED, gen_kind=gen[0], gen_mask=gen[1], offset=offset,
-                       stream=torch.cuda.current_stream().cuda_stream, interp=interp)
+                       stream=torch.cuda.current_stream().cuda_stream, mode=_m(mode))
     torch.cuda.synchronize()
     return out.cpu().numpy(), st.cpu().numpy(), sp.cpu().numpy().view(np.uint32), stats.cpu().numpy()
 
 
-def test_device_api_input_kinds_agree(gpu):
+@pytest.mark.parametrize("mode", MODES)
+def test_device_api_input_kinds_agree(gpu, mode):
     import torch
 
     nodes = mk.networks.sample_network()
     net = mk.Network(nodes)
     n = 100003
     x64 = po.gen_inputs(SEED, n, offset=777)
-    a = _device_run(net, n, offset=777)
-    b = _device_run(net, n, in_tensor=torch.from_numpy(x64.astype(np.int32)).cuda(), in_kind=N.MK_IN_I32)
-    c = _device_run(net, n, in_tensor=torch.from_numpy(x64).cuda(), in_kind=N.MK_IN_I64)
+    a = _device_run(net, n, offset=777, mode=_m(mode))
+    b = _device_run(net, n, in_tensor=torch.from_numpy(x64.astype(np.int32)).cuda(), in_kind=N.MK_IN_I32, mode=_m(mode))
+    c = _device_run(net, n, in_tensor=torch.from_numpy(x64).cuda(), in_kind=N.MK_IN_I64, mode=_m(mode))
+    # misaligned int32 input / output views take the scalar tile path
+    xt = torch.from_numpy(x64.astype(np.int32)).cuda()
+    xo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+    xo[1:] = xt
+    d = _device_run(net, n, in_tensor=xo[1:], in_kind=N.MK_IN_I32, mode=_m(mode))
     ref = oracle(nodes, x64)
-    for r in (a, b, c):
+    for r in (a, b, c, d):
         for u, v in zip(r[:3], ref):
             assert np.array_equal(u, v)
         assert r[3][0] == int(ref[2].sum()) and r[3][2] == n
         assert r[3][1] == int(((ref[1] & 0x10) != 0).sum())
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_c2_full_size_properties(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_c2_full_size_properties(gpu, mode):
     # BASELINE config 2: 16,777,216 lanes; size-independent checks:
     # out == int32(x + 2) (README.md:39-44), 12 retired instrs, quiescent + output.
     import torch
@@ -189,7 +213,7 @@ def test_c2_full_size_properties(gpu, interp):
     net = mk.Network(mk.networks.example_network())
     x = torch.empty(n, dtype=torch.int32, device="cuda")
     mk.generate_inputs_device(n, x.data_ptr(), seed=SEED, stream=torch.cuda.current_stream().cuda_stream)
-    out, st, sp, stats = _device_run(net, n, in_tensor=x, interp=interp)
+    out, st, sp, stats = _device_run(net, n, in_tensor=x, mode=_m(mode))
     xe = x.cpu().numpy().astype(np.int64)
     assert np.array_equal(out, ((xe + 2 + 2**31) % 2**32 - 2**31).astype(np.int32))
     assert (st == 0x11).all() and (sp == 12).all()
@@ -200,15 +224,15 @@ def test_c2_full_size_properties(gpu, interp):
     assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_c3_64m_shard_properties(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_c3_64m_shard_properties(gpu, mode):
     # BASELINE config 3 shards 67,108,864 lanes over 8 GPUs; one shard here
     # (lanes [7*8M, 8*8M)) with the global lane offset of rank 7.
     n = 1 << 23
     off = 7 * n
     nodes = mk.networks.sample_network()
     net = mk.Network(nodes)
-    out, st, sp, stats = _device_run(net, n, offset=off, interp=interp)
+    out, st, sp, stats = _device_run(net, n, offset=off, mode=_m(mode))
     x = po.gen_inputs(SEED, n, offset=off)
     x32 = x.astype(np.int32).astype(np.int64)
     want = ((2 * x32 + 2**31) % 2**32 - 2**31).astype(np.int32)
@@ -222,12 +246,12 @@ def test_c3_64m_shard_properties(gpu, interp):
             assert (sp[cls] == oracle(nodes, x[i:i + 1])[2][0]).all()
 
 
-@pytest.mark.parametrize("interp", TIERS)
-def test_wide_immediates_on_symbolic_acc(gpu, interp):
+@pytest.mark.parametrize("mode", MODES)
+def test_wide_immediates_on_symbolic_acc(gpu, mode):
     # immediates whose low 32-bit word has bit 31 set, applied to a data-dependent ACC
     prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
             "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
             "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
     nodes = [("n", "program", prog)]
     xs = po.gen_inputs(SEED, 4096)
-    assert_same(mk.Network(nodes).compute_batch(xs, interp=interp), oracle(nodes, xs), "wide imm")
+    assert_same(mk.Network(nodes).compute_batch(xs, mode=_m(mode)), oracle(nodes, xs), "wide imm")

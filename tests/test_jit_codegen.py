@@ -1,0 +1,125 @@
+"""Tier 3 (native kernel per network, misaka-net_amd/csrc/tis_jit.cpp) on CPU.
+
+The generator emits the lane function as portable C++; here it is compiled
+with g++ (all networks of a case list into one shared object) and run lane by
+lane against the oracle -- bit-exact out/status/steps.  The GPU runs the same
+function inside the hiprtc-compiled kernel (tests/test_gpu_parity.py, mode
+"jit"); that the full module compiles for gfx950 is checked here too (hiprtc
+needs no GPU)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import misaka_net_amd as mk
+from oracle import pyoracle as po
+import schedcheck as sc
+from tisgen import random_network
+
+SEED = 0x4D49534B41
+
+HEADER = """#include <cstdint>
+#include <cstddef>
+#include <vector>
+#define MK_FN static inline
+"""
+
+
+def build_lanes(cases, path):
+    """cases: [(lane source, nslots)] -> CDLL exporting run<i>(in, n, budget, out, st, steps)."""
+    parts = [HEADER]
+    for i, (src, nslots) in enumerate(cases):
+        parts.append(f"namespace n{i} {{\n{src}\n}}\n")
+        parts.append(
+            f'extern "C" void run{i}(const int64_t *in, size_t n, uint32_t budget, int32_t *out, uint8_t *st,'
+            f" uint32_t *sp) {{\n"
+            f"    std::vector<int32_t> slots({nslots} + 1, 0x5A5A5A5A);\n"
+            f"    for (size_t i = 0; i < n; i++) {{\n"
+            f"        uint32_t s, t;\n"
+            f"        const int32_t o = n{i}::mk_lane(in[i], budget, slots.data(), 1, &s, &t);\n"
+            f"        out[i] = (t & 0x10) ? o : 0; st[i] = (uint8_t)t; sp[i] = s;\n"
+            f"    }}\n}}\n")
+    src = path + ".cpp"
+    with open(src, "w") as f:
+        f.write("".join(parts))
+    so = path + ".so"
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-w", "-o", so, src])
+    return C.CDLL(so)
+
+
+def run_lane(lib, i, xs, budget):
+    v = np.ascontiguousarray(np.asarray(xs, dtype=np.int64))
+    out = np.zeros(v.size, np.int32)
+    st = np.zeros(v.size, np.uint8)
+    sp = np.zeros(v.size, np.uint32)
+    getattr(lib, f"run{i}")(C.c_void_p(v.ctypes.data), C.c_size_t(v.size), C.c_uint32(budget),
+                            C.c_void_p(out.ctypes.data), C.c_void_p(st.ctypes.data), C.c_void_p(sp.ctypes.data))
+    return out, st, sp
+
+
+def check_cases(tmp_path, cases):
+    """cases: [(label, nodes, xs, kw)] -- every case compiled and compared."""
+    srcs, keep = [], []
+    for label, nodes, xs, kw in cases:
+        try:
+            src, ns = sc.jit_lane(nodes, stack_cap=kw.get("stack_cap"), stop_on_output=kw.get("stop_on_output", False))
+        except sc.NotCompiled:
+            continue  # tier 1 handles it; covered elsewhere
+        srcs.append((src, ns))
+        keep.append((label, nodes, xs, kw))
+    assert keep, "no case compiled"
+    lib = build_lanes(srcs, str(tmp_path / "lanes"))
+    for i, (label, nodes, xs, kw) in enumerate(keep):
+        got = run_lane(lib, i, xs, kw.get("budget") or (1 << 20))
+        ref = po.OracleNet(nodes).compute_batch(xs, **kw)
+        bad = np.nonzero((got[0] != ref[0]) | (got[1] != ref[1]) | (got[2] != ref[2]))[0]
+        assert not bad.size, (label, int(bad[0]), [g[bad[0]] for g in got], [r[bad[0]] for r in ref])
+    return [k[0] for k in keep]
+
+
+def test_configs(tmp_path):
+    cases = []
+    for name in sorted(mk.networks.CONFIGS):
+        kind = 1 if name.startswith("c5") else 0
+        cases.append((name, mk.networks.CONFIGS[name](), po.gen_inputs(SEED, 2000, kind=kind, mask=1023), {}))
+    cases.append(("c4_d1024", mk.networks.pipeline_network(1024), po.gen_inputs(SEED, 40), {}))
+    cases.append(("c5_all_trips", mk.networks.countdown_network(), np.arange(0, 1024, dtype=np.int64), {}))
+    for b in (1, 11, 12, 13):
+        cases.append((f"c2_budget{b}", mk.networks.example_network(), po.gen_inputs(SEED, 300), {"budget": b}))
+        cases.append((f"c5_budget{b}", mk.networks.countdown_network(),
+                      po.gen_inputs(SEED, 300, kind=1, mask=1023), {"budget": b * 37}))
+    done = check_cases(tmp_path, cases)
+    # the deep pipelines exceed the native tier's size limit (tier 2 runs them)
+    assert set(c[0] for c in cases) - set(done) == {"c4_pipeline", "c4_d1024"}
+
+
+def test_wide_immediates_and_stop(tmp_path):
+    prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
+            "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
+            "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
+    loop = [("a", "program", "JRO 0"), ("b", "program", "OUT 3\nJRO 0")]
+    cases = [("wide", [("n", "program", prog)], po.gen_inputs(SEED, 2048), {}),
+             ("budget", loop, [0] * 8, {"budget": 11}),
+             ("stop", loop, [0] * 8, {"stop_on_output": True})]
+    assert len(check_cases(tmp_path, cases)) == 3
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_networks(tmp_path, block):
+    cases = []
+    for seed in range(block * 40, block * 40 + 40):
+        kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=[1, 3, 8, 16, 17, 40, 1024][seed % 7],
+                  stop_on_output=(seed % 5 == 4))
+        cases.append((f"seed{seed}", random_network(seed), po.gen_inputs(seed * 7919 + 1, 256), kw))
+    assert len(check_cases(tmp_path, cases)) >= 30
+
+
+def test_module_compiles_for_gfx950():
+    # hiprtc in-process, no GPU: the product library reports the native tier
+    net = mk.Network(mk.networks.countdown_network())
+    plan = net.plan(mode="jit")
+    assert plan.startswith("tier=native "), plan
+    src = net.jit_source()
+    assert "mk_jit_exec" in src and "mk_lane" in src
