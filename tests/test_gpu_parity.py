@@ -99,9 +99,9 @@ def test_random_networks_bit_exact(gpu, seed, mode):
     kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=cap, stop_on_output=(seed % 5 == 4))
     net = mk.Network(rows)
     got = net.compute_batch(xs, mode=_m(mode), **kw)
-    if mode == "auto":  # the default path really is the native tier for these small networks
+    if mode == "auto":  # the default path is the native tier unless a limit sends it down a tier, with a reason
         plan = net.plan(stack_cap=kw["stack_cap"], stop_on_output=kw["stop_on_output"])
-        assert plan.startswith(("tier=native", "tier=interp")), plan
+        assert plan.startswith(("tier=native", "tier=interp")) or " native=" in plan, plan
     assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
 
 
