@@ -821,6 +821,7 @@ struct JitState {
     std::vector<char> code;   // gfx950 code object
     double compile_s = 0;
     size_t src_bytes = 0;
+    JitShape shape = JIT_STREAM;
     JitDev dev[kMaxDevices];
 };
 
@@ -1158,8 +1159,11 @@ bool jit_compile(SchedCache *sc)
     }
     const auto t0 = std::chrono::steady_clock::now();
     std::string lane;
-    if (!jit_lane_source(sc->prog, JitLimits{}, lane, J.why)) return false;
-    const std::string src = jit_module_source(lane);
+    JitLimits lim;
+    const char *shp = std::getenv("MK_JIT_SHAPE"); // "machine": force the machine shape (experiments)
+    lim.force_machine = shp && std::strcmp(shp, "machine") == 0;
+    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape)) return false;
+    const std::string src = jit_module_source(lane, J.shape);
     J.src_bytes = src.size();
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
@@ -1205,6 +1209,17 @@ int ensure_jit_device(SchedCache *sc, int d)
     return MK_OK;
 }
 
+// Machine-shape policy word (tis_jit.h kJitPolicy); MK_JIT_POLICY="refill,num,min"
+// overrides it for experiments.
+uint32_t jit_policy()
+{
+    const char *env = std::getenv("MK_JIT_POLICY");
+    unsigned r = 0, nu = 0, mi = 0;
+    if (env && std::sscanf(env, "%u,%u,%u", &r, &nu, &mi) == 3 && r <= 64 && nu <= 16 && mi <= 64)
+        return r | nu << 8 | mi << 16;
+    return kJitPolicy;
+}
+
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
 int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, hipStream_t stream)
@@ -1216,7 +1231,8 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     JitDev &jd = sc->jit.dev[d];
     const SchedProgram &P = sc->prog;
     DeviceGuard g(d);
-    const uint64_t want = (n + kJitBlock - 1) / kJitBlock;
+    const uint64_t per_block = sc->jit.shape == JIT_STREAM ? (uint64_t)kJitBlock * kJitStreamLanes : kJitBlock;
+    const uint64_t want = (n + per_block - 1) / per_block;
     const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
     const uint64_t lanes = (uint64_t)blocks * kJitBlock;
@@ -1250,6 +1266,10 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     p.slots = P.nslots ? sd.d_slots : nullptr;
     p.lanes = lanes;
     p.vlanes = lanes;
+    const uintptr_t va = 4u * kJitStreamLanes;
+    p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
+               (uintptr_t)d_status % kJitStreamLanes == 0 && (uintptr_t)d_steps % va == 0;
+    p.policy = jit_policy();
     void *args[] = {(void *)&p};
     if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, kJitBlock, 1, 1, 0, stream, args, nullptr) != hipSuccess)
         return MK_EDEVICE;
@@ -1558,7 +1578,8 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     std::string s;
     if (t == mk::TIER_NATIVE) {
         char tail[160];
-        snprintf(tail, sizeof tail, " source=%zuB code=%zuB compile=%.2fs", sc->jit.src_bytes, sc->jit.code.size(),
+        snprintf(tail, sizeof tail, " shape=%s source=%zuB code=%zuB compile=%.2fs",
+                 sc->jit.shape == mk::JIT_MACHINE ? "machine" : "stream", sc->jit.src_bytes, sc->jit.code.size(),
                  sc->jit.compile_s);
         s = std::string("tier=native ") + buf + tail;
     } else {
@@ -1598,7 +1619,11 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     mk::SchedCache *sc = mk::get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
     std::string lane, why;
     if (!sc->ok) why = sc->why;
-    else if (mk::jit_lane_source(sc->prog, mk::JitLimits{}, lane, why)) return mk::copy_out(out, out_len, mk::jit_module_source(lane));
+    else {
+        mk::JitShape shape;
+        if (mk::jit_lane_source(sc->prog, mk::JitLimits{}, lane, why, &shape))
+            return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape));
+    }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;
 }

@@ -148,18 +148,23 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
 // Lane function of the native tier (tis_jit.h) for the CPU tests: returns 0
 // with the source in `out`, 1 when the schedule or the JIT declined (why in
 // `out`), negative when `out` is too small.
-int mkc_jit_lane(void *hv, uint32_t cap, int soo, uint32_t *nslots, char *out, size_t out_len)
+int mkc_jit_lane(void *hv, uint32_t cap, int soo, int force_machine, uint32_t *nslots, int *shape, char *out,
+                 size_t out_len)
 {
     auto *h = (CheckNet *)hv;
     mk::SchedProgram P;
     std::string w, src;
     mk::SchedLimits lim;
+    mk::JitLimits jl;
+    jl.force_machine = force_machine != 0;
+    mk::JitShape sh = mk::JIT_STREAM;
     int rc = 0;
-    if (!mk::compile_schedule(h->net, cap, soo != 0, lim, P, w) || !mk::jit_lane_source(P, mk::JitLimits{}, src, w)) {
+    if (!mk::compile_schedule(h->net, cap, soo != 0, lim, P, w) || !mk::jit_lane_source(P, jl, src, w, &sh)) {
         src = w;
         rc = 1;
     }
     *nslots = P.nslots;
+    *shape = (int)sh;
     if (src.size() + 1 > out_len) return -1;
     memcpy(out, src.c_str(), src.size() + 1);
     return rc;

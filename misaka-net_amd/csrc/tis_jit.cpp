@@ -7,6 +7,16 @@
 // register stride, so register r has operand r*8) -- the same stream the
 // tier-2 kernel interprets and the host model in sched_check.cpp executes --
 // and each micro-op is restated exactly as those two execute it.
+//
+// Two shapes of generated code (tis_jit.h):
+//   stream  -- the reachable superblock graph is acyclic: every lane runs a
+//              bounded straight-line path, so the kernel streams tiles of 4
+//              lanes per thread with vector I/O (HBM-bound networks);
+//   machine -- the graph has cycles (loops whose trip counts follow the
+//              data): each thread holds one lane as a small state machine
+//              (superblock id + registers), a wave-uniform dispatcher runs
+//              one superblock at a time for the lanes sitting on it, and a
+//              lane that ends takes its next input while the others go on.
 #include "tis_jit.h"
 
 #include <cinttypes>
@@ -31,7 +41,7 @@ struct Emitter {
     std::string s;
     void line(const char *fmt, ...) __attribute__((format(printf, 2, 3)))
     {
-        char buf[512];
+        char buf[1024];
         va_list ap;
         va_start(ap, fmt);
         vsnprintf(buf, sizeof buf, fmt, ap);
@@ -41,18 +51,6 @@ struct Emitter {
     }
 };
 
-// Operand A/B: register value, sign-extended from its low 32 bits when the
-// micro-op says so (UF_TA / UF_TB).
-std::string operand(uint32_t off, bool trunc)
-{
-    char b[64];
-    if (trunc)
-        snprintf(b, sizeof b, "((int64_t)(int32_t)r%u)", off / 8);
-    else
-        snprintf(b, sizeof b, "r%u", off / 8);
-    return b;
-}
-
 std::string u64lit(int64_t v)
 {
     char b[32];
@@ -60,36 +58,35 @@ std::string u64lit(int64_t v)
     return b;
 }
 
-std::string result(const DOp &I)
-{
-    if (I.fl & UF_OUTREG) return "(int32_t)" + operand(I.a, I.fl & UF_TA);
-    char b[48];
-    snprintf(b, sizeof b, "(int32_t)%" PRId32, (int32_t)I.imm);
-    return b;
-}
-
-} // namespace
-
-bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why)
-{
+// The reachable part of a schedule's device form.
+struct Graph {
+    std::vector<DOp> D;
     std::vector<uint32_t> entry;
-    const std::vector<DOp> D = assemble_device(p, 8, entry);
-    const size_t nv = entry.size();
+    std::vector<char> seen;      // variant reachable from variant 0
+    std::vector<char> used_reg;  // register read or written by reachable code
+    size_t nreach = 0, ndops = 0;
+    bool cyclic = false;
+};
+
+bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string &why)
+{
+    g.D = assemble_device(p, 8, g.entry);
+    const size_t nv = g.entry.size();
     if (nv == 0) {
         why = "empty schedule";
         return false;
     }
-    // reachable variants from variant 0 (the entry superblock, fast variant)
-    std::vector<char> seen(nv, 0);
+    g.seen.assign(nv, 0);
+    g.used_reg.assign(p.nregs + 1, 0);
+    g.used_reg[p.in_reg] = 1;
+    std::vector<std::vector<uint32_t>> succ(nv);
     std::deque<uint32_t> work{0};
-    seen[0] = 1;
-    size_t nreach = 0, ndops = 0;
-    std::vector<char> used_reg(p.nregs + 1, 0);
-    used_reg[p.in_reg] = 1;
-    auto reach = [&](uint64_t v) -> bool {
+    g.seen[0] = 1;
+    auto reach = [&](uint32_t from, uint64_t v) -> bool {
         if (v >= nv) return false;
-        if (!seen[v]) {
-            seen[v] = 1;
+        succ[from].push_back((uint32_t)v);
+        if (!g.seen[v]) {
+            g.seen[v] = 1;
             work.push_back((uint32_t)v);
         }
         return true;
@@ -97,22 +94,22 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     while (!work.empty()) {
         const uint32_t v = work.front();
         work.pop_front();
-        if (++nreach > lim.max_variants) {
+        if (++g.nreach > lim.max_variants) {
             why = "too many superblock variants for the native tier";
             return false;
         }
-        for (size_t pc = entry[v];; ++pc) {
-            if (pc >= D.size()) {
+        for (size_t pc = g.entry[v];; ++pc) {
+            if (pc >= g.D.size()) {
                 why = "superblock runs off the code";
                 return false;
             }
-            if (++ndops > lim.max_dops) {
+            if (++g.ndops > lim.max_dops) {
                 why = "schedule too large for the native tier";
                 return false;
             }
-            const DOp &I = D[pc];
+            const DOp &I = g.D[pc];
             auto use = [&](uint32_t off) {
-                if (off / 8 < used_reg.size()) used_reg[off / 8] = 1;
+                if (off / 8 < g.used_reg.size()) g.used_reg[off / 8] = 1;
             };
             bool leave = false, ok = true;
             switch (I.op) {
@@ -121,22 +118,22 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
             case U_LI: case U_LD: use(I.d); break;
             case U_ST: use(I.a); break;
             case U_STI: break;
-            case U_JUMP: ok = reach((uint64_t)I.imm); leave = true; break;
+            case U_JUMP: ok = reach(v, (uint64_t)I.imm); leave = true; break;
             case U_BR:
                 use(I.a);
-                ok = reach((uint32_t)(uint64_t)I.imm) && reach((uint64_t)I.imm >> 32);
+                ok = reach(v, (uint32_t)(uint64_t)I.imm) && reach(v, (uint64_t)I.imm >> 32);
                 leave = true;
                 break;
             case U_JRO:
                 use(I.a);
                 for (uint64_t t = 0; t <= I.b && ok; ++t) {
                     const uint64_t j = (uint64_t)I.imm + t;
-                    ok = j < p.jtab.size() && reach(p.jtab[j]);
+                    ok = j < p.jtab.size() && reach(v, p.jtab[j]);
                 }
                 leave = true;
                 break;
             case U_END: if (I.fl & UF_OUTREG) use(I.a); leave = true; break;
-            case U_GUARD: ok = reach((uint64_t)I.imm); break;
+            case U_GUARD: ok = reach(v, (uint64_t)I.imm); break;
             case U_ROUND_END: if (I.fl & UF_OUTREG) use(I.a); break;
             default: ok = false;
             }
@@ -147,67 +144,132 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
             if (leave) break;
         }
     }
-    for (uint32_t r = 0; r < used_reg.size(); ++r)
-        if (used_reg[r] && r >= p.nregs) {
+    for (uint32_t r = 0; r < g.used_reg.size(); ++r)
+        if (g.used_reg[r] && r >= p.nregs) {
             why = "register out of range";
             return false;
         }
+    // cycle detection over reachable variants (iterative DFS, colours 0/1/2)
+    std::vector<uint8_t> col(nv, 0);
+    std::vector<std::pair<uint32_t, size_t>> st{{0u, 0}};
+    col[0] = 1;
+    while (!st.empty() && !g.cyclic) {
+        auto &[v, k] = st.back();
+        if (k < succ[v].size()) {
+            const uint32_t w = succ[v][k++];
+            if (col[w] == 1) g.cyclic = true;
+            else if (col[w] == 0) {
+                col[w] = 1;
+                st.push_back({w, 0});
+            }
+        } else {
+            col[v] = 2;
+            st.pop_back();
+        }
+    }
+    return true;
+}
 
-    Emitter e;
-    e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops", nreach, ndops);
+// Micro-op emission shared by both shapes.  `R` prefixes register names
+// ("r" for locals of the stream lane function, "L.r" for the machine's lane
+// state); `exit_*` print the shape's form of each superblock exit.
+struct OpWriter {
+    Emitter &e;
+    const SchedProgram &p;
+    const char *R;
+
+    std::string operand(uint32_t off, bool trunc) const
+    {
+        char b[64];
+        if (trunc)
+            snprintf(b, sizeof b, "((int64_t)(int32_t)%s%u)", R, off / 8);
+        else
+            snprintf(b, sizeof b, "%s%u", R, off / 8);
+        return b;
+    }
+
+    std::string result(const DOp &I) const
+    {
+        if (I.fl & UF_OUTREG) return "(int32_t)" + operand(I.a, I.fl & UF_TA);
+        char b[48];
+        snprintf(b, sizeof b, "(int32_t)%" PRId32, (int32_t)I.imm);
+        return b;
+    }
+
+    std::string cond(const DOp &I) const
+    {
+        static const char *const cmp[4] = {"== 0", "!= 0", "> 0", "< 0"};
+        return "(" + operand(I.a, I.fl & UF_TA) + " " + cmp[(I.fl >> UF_COND_SHIFT) & 3u] + ")";
+    }
+
+    // Data micro-ops; returns false for an exit / control op.
+    bool data(const DOp &I) const
+    {
+        const std::string A = operand(I.a, I.fl & UF_TA), B = operand(I.b, I.fl & UF_TB);
+        const uint32_t d = I.d / 8;
+        switch (I.op) {
+        case U_MOV: e.line("    %s%u = %s;", R, d, A.c_str()); return true;
+        case U_LI: e.line("    %s%u = (int64_t)%s;", R, d, u64lit(I.imm).c_str()); return true;
+        case U_ADD: e.line("    %s%u = (int64_t)((uint64_t)%s + (uint64_t)%s);", R, d, A.c_str(), B.c_str()); return true;
+        case U_SUB: e.line("    %s%u = (int64_t)((uint64_t)%s - (uint64_t)%s);", R, d, A.c_str(), B.c_str()); return true;
+        case U_ADDI: e.line("    %s%u = (int64_t)((uint64_t)%s + %s);", R, d, A.c_str(), u64lit(I.imm).c_str()); return true;
+        case U_RSUBI: e.line("    %s%u = (int64_t)(%s - (uint64_t)%s);", R, d, u64lit(I.imm).c_str(), A.c_str()); return true;
+        case U_ST: e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%s;", (uint32_t)I.imm, A.c_str()); return true;
+        case U_STI:
+            e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%" PRId32 ";", I.d, (int32_t)I.imm);
+            return true;
+        case U_LD: e.line("    %s%u = (int64_t)slots[(uint64_t)%uu * sstride];", R, d, (uint32_t)I.imm); return true;
+        default: return false;
+        }
+    }
+
+    // t = IntClamp(ip + A, 0, len-1) with an int64 wrapping add (program.go:354,362)
+    void jro_target(const DOp &I) const
+    {
+        e.line("        int64_t t = (int64_t)((uint64_t)%uu + (uint64_t)%s);", I.d, operand(I.a, I.fl & UF_TA).c_str());
+        e.line("        t = t > (int64_t)%u ? (int64_t)%u : t;", I.b, I.b);
+        e.line("        t = t < 0 ? 0 : t;");
+    }
+};
+
+// ---- stream shape: straight-line lane function ------------------------------
+
+void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e)
+{
+    OpWriter w{e, p, "r"};
+    const size_t nv = g.entry.size();
+    e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
+    e.line("#define MK_JIT_MACHINE 0");
     e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
     e.line("{");
     for (uint32_t r = 0; r < p.nregs; ++r)
-        if (used_reg[r]) e.line("    int64_t r%u = 0;", r);
+        if (g.used_reg[r]) e.line("    int64_t r%u = 0;", r);
     e.line("    r%u = (int64_t)(int32_t)in;", p.in_reg);
     e.line("    uint32_t steps = 0, st = 0;");
     e.line("    int32_t outv = 0;");
     e.line("    (void)slots; (void)sstride; (void)budget;");
     for (uint32_t v = 0; v < nv; ++v) {
-        if (!seen[v]) continue;
+        if (!g.seen[v]) continue;
         e.line("V%u:", v);
-        for (size_t pc = entry[v];; ++pc) {
-            const DOp &I = D[pc];
-            const bool ta = I.fl & UF_TA, tb = I.fl & UF_TB;
-            const std::string A = operand(I.a, ta), B = operand(I.b, tb);
-            const uint32_t d = I.d / 8;
-            bool leave = false;
+        for (size_t pc = g.entry[v];; ++pc) {
+            const DOp &I = g.D[pc];
+            if (w.data(I)) continue;
+            bool leave = true;
             switch (I.op) {
-            case U_MOV: e.line("    r%u = %s;", d, A.c_str()); break;
-            case U_LI: e.line("    r%u = (int64_t)%s;", d, u64lit(I.imm).c_str()); break;
-            case U_ADD: e.line("    r%u = (int64_t)((uint64_t)%s + (uint64_t)%s);", d, A.c_str(), B.c_str()); break;
-            case U_SUB: e.line("    r%u = (int64_t)((uint64_t)%s - (uint64_t)%s);", d, A.c_str(), B.c_str()); break;
-            case U_ADDI: e.line("    r%u = (int64_t)((uint64_t)%s + %s);", d, A.c_str(), u64lit(I.imm).c_str()); break;
-            case U_RSUBI: e.line("    r%u = (int64_t)(%s - (uint64_t)%s);", d, u64lit(I.imm).c_str(), A.c_str()); break;
-            case U_ST:
-                e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%s;", (uint32_t)I.imm, A.c_str());
-                break;
-            case U_STI:
-                e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%" PRId32 ";", I.d, (int32_t)I.imm);
-                break;
-            case U_LD: e.line("    r%u = (int64_t)slots[(uint64_t)%uu * sstride];", d, (uint32_t)I.imm); break;
             case U_JUMP:
                 e.line("    steps += %uu;", I.inc);
                 e.line("    goto V%u;", (uint32_t)I.imm);
-                leave = true;
                 break;
-            case U_BR: {
-                static const char *const cmp[4] = {"== 0", "!= 0", "> 0", "< 0"};
-                const uint32_t c = (I.fl >> UF_COND_SHIFT) & 3u;
+            case U_BR:
                 e.line("    steps += %uu;", I.inc);
-                e.line("    if (%s %s) goto V%u;", A.c_str(), cmp[c], (uint32_t)(uint64_t)I.imm);
+                e.line("    if %s goto V%u;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm);
                 e.line("    goto V%u;", (uint32_t)((uint64_t)I.imm >> 32));
-                leave = true;
                 break;
-            }
             case U_JRO: {
-                // IntClamp(ip + A, 0, len-1) with an int64 wrapping add (program.go:354,362)
                 e.line("    steps += %uu;", I.inc);
                 e.line("    {");
-                e.line("        int64_t t = (int64_t)((uint64_t)%uu + (uint64_t)%s);", I.d, A.c_str());
-                e.line("        t = t > (int64_t)%u ? (int64_t)%u : t;", I.b, I.b);
-                e.line("        t = t < 0 ? 0 : t;");
+                w.jro_target(I);
                 e.line("        switch (t) {");
                 const uint32_t last = p.jtab[(size_t)I.imm + I.b];
                 for (uint32_t t = 0; t < I.b; ++t) {
@@ -217,27 +279,28 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
                 e.line("        default: goto V%u;", last);
                 e.line("        }");
                 e.line("    }");
-                leave = true;
                 break;
             }
             case U_END:
                 e.line("    steps += %uu;", I.inc);
-                e.line("    outv = %s;", result(I).c_str());
+                e.line("    outv = %s;", w.result(I).c_str());
                 e.line("    st = %uu;", I.d);
                 e.line("    goto done;");
-                leave = true;
                 break;
             case U_GUARD:
                 e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", I.inc, (uint32_t)I.imm);
+                leave = false;
                 break;
             case U_ROUND_END:
                 e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) {", I.inc);
                 e.line("        steps += %uu;", I.inc);
-                e.line("        outv = %s;", result(I).c_str());
+                e.line("        outv = %s;", w.result(I).c_str());
                 e.line("        st = %uu;", I.d);
                 e.line("        goto done;");
                 e.line("    }");
+                leave = false;
                 break;
+            default: break;
             }
             if (leave) break;
         }
@@ -247,11 +310,376 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     e.line("    *status_out = st;");
     e.line("    return outv;");
     e.line("}");
+}
+
+// ---- machine shape: resumable lane --------------------------------------------
+
+// A fast variant that loops on itself: GUARD, data micro-ops, then BR or JUMP
+// with itself as a target (emit_self_loop).
+bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
+{
+    if (v & 1u) return false;
+    size_t pc = g.entry[v];
+    if (g.D[pc].op != U_GUARD) return false;
+    guard_pc = pc++;
+    for (;; ++pc) {
+        const DOp &I = g.D[pc];
+        switch (I.op) {
+        case U_MOV: case U_LI: case U_ADD: case U_SUB: case U_ADDI: case U_RSUBI: case U_ST: case U_STI: case U_LD:
+            continue;
+        case U_JUMP:
+            exit_pc = pc;
+            return (uint32_t)I.imm == v;
+        case U_BR:
+            exit_pc = pc;
+            return (uint32_t)(uint64_t)I.imm == v || (uint32_t)((uint64_t)I.imm >> 32) == v;
+        default: return false;
+        }
+    }
+}
+
+// Self-loop v as a wave-uniform loop with per-lane predication.  The lanes
+// of the group run the body together; a lane's flag `a` drops once it leaves
+// the loop (branch not taken, or the next iteration's budget guard fails) and
+// from then on its registers and steps stay frozen (selects), so the loop
+// control is scalar and no divergent branch or exec-mask bookkeeping is paid
+// per iteration -- only the body, the selects and two compares.  The wave
+// checks every MK_UNROLL iterations whether enough of the group is still in
+// the loop (MK_KEEP), so a few long trips do not hold the others.
+constexpr int kLoopUnroll = 4;
+
+void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
+{
+    Emitter &e = w.e;
+    const DOp &G = g.D[gpc], &X = g.D[xpc];
+    // registers the body reads or writes, and the ones it writes
+    std::vector<char> rd(g.used_reg.size(), 0), wr(g.used_reg.size(), 0);
+    auto R = [&](uint32_t off) { rd[off / 8] = 1; };
+    auto W = [&](uint32_t off) { wr[off / 8] = rd[off / 8] = 1; };
+    bool stores = false;
+    for (size_t pc = gpc + 1; pc < xpc; ++pc) {
+        const DOp &I = g.D[pc];
+        switch (I.op) {
+        case U_MOV: case U_ADDI: case U_RSUBI: R(I.a); W(I.d); break;
+        case U_ADD: case U_SUB: R(I.a); R(I.b); W(I.d); break;
+        case U_LI: case U_LD: W(I.d); break;
+        case U_ST: R(I.a); stores = true; break;
+        case U_STI: stores = true; break;
+        default: break;
+        }
+    }
+    std::string c = "true";
+    uint32_t other = v;
+    if (X.op == U_BR) {
+        R(X.a);
+        const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
+        OpWriter n{e, w.p, "n"};
+        if (tk == v && nt != v) c = n.cond(X), other = nt;
+        else if (tk != v) c = "!" + n.cond(X), other = tk;
+    }
+    // guard: steps + g >= budget  <=>  steps >= lim (lim = 0 when budget <= g)
+    e.line("    const uint32_t lim = budget > %uu ? budget - %uu : 0u;", G.inc, G.inc);
+    e.line("    if (L.steps >= lim) {");
+    e.line("        L.sb = %uu;", (uint32_t)G.imm);
+    e.line("        break;");
+    e.line("    }");
+    e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
+    e.line("    bool a = true;");
+    e.line("    do {");
+    for (int u = 0; u < kLoopUnroll; ++u) {
+        e.line("    {");
+        for (uint32_t r = 0; r < rd.size(); ++r)
+            if (rd[r]) e.line("    int64_t n%u = L.r%u;", r, r);
+        OpWriter n{e, w.p, "n"};
+        for (size_t pc = gpc + 1; pc < xpc; ++pc) {
+            const DOp &I = g.D[pc];
+            if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
+            n.data(I);
+        }
+        for (uint32_t r = 0; r < wr.size(); ++r)
+            if (wr[r]) e.line("    L.r%u = a ? n%u : L.r%u;", r, r, r);
+        e.line("    L.steps += a ? %uu : 0u;", X.inc);
+        e.line("    a = a & (%s) & (L.steps < lim);", c.c_str());
+        e.line("    }");
+    }
+    e.line("    } while (MK_KEEP(a, need));");
+    // a: still in the loop (suspended); otherwise it left through the branch
+    // (the condition on its frozen registers fails) or through the guard
+    OpWriter l{e, w.p, "L.r"};
+    std::string cl = "true";
+    if (X.op == U_BR) {
+        const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
+        if (tk == v && nt != v) cl = l.cond(X);
+        else if (tk != v) cl = "!" + l.cond(X);
+    }
+    e.line("    L.sb = (a || (%s)) ? (L.steps < lim ? %uu : %uu) : %uu;", cl.c_str(), v, (uint32_t)G.imm, other);
+    e.line("    break;");
+    e.line("    }");
+    (void)stores;
+}
+
+void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
+{
+    OpWriter w{e, p, "L.r"};
+    const size_t nv = g.entry.size();
+    size_t nloops = 0;
+    e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
+    e.line("#define MK_JIT_MACHINE 1");
+    e.line("#define MK_SB_DONE 0xFFFFFFFEu");
+    e.line("#define MK_SB_IDLE 0xFFFFFFFFu");
+    e.line("struct MkLane {");
+    for (uint32_t r = 0; r < p.nregs; ++r)
+        if (g.used_reg[r]) e.line("    int64_t r%u;", r);
+    e.line("    uint32_t sb, steps, st;");
+    e.line("    int32_t outv;");
+    e.line("};");
+    e.line("MK_FN void mk_init(MkLane &L, int64_t in)");
+    e.line("{");
+    for (uint32_t r = 0; r < p.nregs; ++r)
+        if (g.used_reg[r]) e.line("    L.r%u = 0;", r);
+    e.line("    L.r%u = (int64_t)(int32_t)in;", p.in_reg);
+    e.line("    L.sb = 0u;");
+    e.line("    L.steps = 0u;");
+    e.line("    L.st = 0u;");
+    e.line("    L.outv = 0;");
+    e.line("}");
+    // mk_run(u, ...): superblock variant u for a lane sitting on it (L.sb == u).
+    // MK_LOOP_NEED() / MK_KEEP(m, need) come from the includer: the wave's
+    // policy for leaving a loop early so that finished lanes can refill.
+    e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
+    e.line("                  const uint64_t sstride, const uint32_t pol)");
+    e.line("{");
+    e.line("    (void)slots; (void)sstride; (void)budget; (void)pol;");
+    e.line("    switch (u) {");
+    for (uint32_t v = 0; v < nv; ++v) {
+        if (!g.seen[v]) continue;
+        e.line("    case %uu: {", v);
+        size_t gpc = 0, xpc = 0;
+        if (self_loop(g, v, gpc, xpc)) {
+            ++nloops;
+            emit_self_loop(w, g, v, gpc, xpc);
+            continue;
+        }
+        for (size_t pc = g.entry[v];; ++pc) {
+            const DOp &I = g.D[pc];
+            if (w.data(I)) continue;
+            bool leave = true;
+            switch (I.op) {
+            case U_JUMP:
+                e.line("    L.steps += %uu;", I.inc);
+                e.line("    L.sb = %uu;", (uint32_t)I.imm);
+                break;
+            case U_BR:
+                e.line("    L.steps += %uu;", I.inc);
+                e.line("    L.sb = %s ? %uu : %uu;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm,
+                       (uint32_t)((uint64_t)I.imm >> 32));
+                break;
+            case U_JRO: {
+                e.line("    L.steps += %uu;", I.inc);
+                e.line("    {");
+                w.jro_target(I);
+                const uint32_t last = p.jtab[(size_t)I.imm + I.b];
+                std::string sel;
+                for (uint32_t t = 0; t < I.b; ++t) {
+                    const uint32_t tgt = p.jtab[(size_t)I.imm + t];
+                    if (tgt == last) continue;
+                    char b[64];
+                    snprintf(b, sizeof b, "t == %u ? %uu : ", t, tgt);
+                    sel += b;
+                }
+                e.line("        L.sb = %s%uu;", sel.c_str(), last);
+                e.line("    }");
+                break;
+            }
+            case U_END:
+                e.line("    L.steps += %uu;", I.inc);
+                e.line("    L.outv = %s;", w.result(I).c_str());
+                e.line("    L.st = %uu;", I.d);
+                e.line("    L.sb = MK_SB_DONE;");
+                break;
+            case U_GUARD:
+                e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", I.inc);
+                e.line("        L.sb = %uu;", (uint32_t)I.imm);
+                e.line("        break;");
+                e.line("    }");
+                leave = false;
+                break;
+            case U_ROUND_END:
+                e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", I.inc);
+                e.line("        L.steps += %uu;", I.inc);
+                e.line("        L.outv = %s;", w.result(I).c_str());
+                e.line("        L.st = %uu;", I.d);
+                e.line("        L.sb = MK_SB_DONE;");
+                e.line("        break;");
+                e.line("    }");
+                leave = false;
+                break;
+            default: break;
+            }
+            if (leave) break;
+        }
+        e.line("    break;");
+        e.line("    }");
+    }
+    e.line("    default: L.sb = MK_SB_DONE; break;");
+    e.line("    }");
+    e.line("}");
+    e.line("// %zu self-loops", nloops);
+    // the whole lane, for the CPU tests (the kernel drives mk_run itself)
+    e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
+    e.line("                      uint32_t *steps_out, uint32_t *status_out)");
+    e.line("{");
+    e.line("    MkLane L;");
+    e.line("    mk_init(L, in);");
+    e.line("    while (L.sb < MK_SB_DONE) mk_run(L.sb, L, budget, slots, sstride, 0u);");
+    e.line("    *steps_out = L.steps;");
+    e.line("    *status_out = L.st;");
+    e.line("    return L.outv;");
+    e.line("}");
+}
+
+} // namespace
+
+bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape)
+{
+    Graph g;
+    if (!analyze(p, lim, g, why)) return false;
+    Emitter e;
+    const JitShape s = lim.force_machine || g.cyclic ? JIT_MACHINE : JIT_STREAM;
+    if (s == JIT_MACHINE)
+        emit_machine_lane(p, g, e);
+    else
+        emit_stream_lane(p, g, e);
+    if (shape) *shape = s;
     src = std::move(e.s);
     return true;
 }
 
-std::string jit_module_source(const std::string &lane_src)
+// Kernel of the stream shape.  A block takes tiles of 4 x 256 contiguous
+// inputs (grid-stride); thread tid owns inputs tile*1024 + tid*4 .. +3,
+// loads the next tile's 16 bytes before running the current 4 lanes one
+// after another, and writes 16 B of out + 4 B of status per tile (+16 B of
+// steps on request).  Counters fold per wave (stats_reduce).
+static const char *const kStreamKernel = R"(
+__device__ __forceinline__ void mk_load4(const SParams &p, uint64_t base, int32_t &a, int32_t &b, int32_t &c, int32_t &d)
+{
+    if (p.io_vec && base + 4 <= p.n) {
+        const int4 q = *reinterpret_cast<const int4 *>((const int32_t *)p.in_data + base);
+        a = q.x, b = q.y, c = q.z, d = q.w;
+        return;
+    }
+    a = base < p.n ? sched_input(p, base) : 0;
+    b = base + 1 < p.n ? sched_input(p, base + 1) : 0;
+    c = base + 2 < p.n ? sched_input(p, base + 2) : 0;
+    d = base + 3 < p.n ? sched_input(p, base + 3) : 0;
+}
+
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
+    const uint64_t tile = 1024u, ntiles = (p.n + tile - 1) / tile;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    int32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
+    uint64_t t = blockIdx.x;
+    if (t < ntiles) mk_load4(p, t * tile + (uint64_t)tid * 4u, x0, x1, x2, x3);
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * tile + (uint64_t)tid * 4u;
+        const int32_t c0 = x0, c1 = x1, c2 = x2, c3 = x3;
+        if (t + gridDim.x < ntiles) mk_load4(p, base + (uint64_t)gridDim.x * tile, x0, x1, x2, x3);
+        uint32_t s0, s1, s2, s3, t0, t1, t2, t3;
+        int32_t o0 = mk_lane(c0, p.budget, slots, p.lanes, &s0, &t0);
+        int32_t o1 = mk_lane(c1, p.budget, slots, p.lanes, &s1, &t1);
+        int32_t o2 = mk_lane(c2, p.budget, slots, p.lanes, &s2, &t2);
+        int32_t o3 = mk_lane(c3, p.budget, slots, p.lanes, &s3, &t3);
+        o0 = (t0 & MK_ST_HAS_OUTPUT) ? o0 : 0;
+        o1 = (t1 & MK_ST_HAS_OUTPUT) ? o1 : 0;
+        o2 = (t2 & MK_ST_HAS_OUTPUT) ? o2 : 0;
+        o3 = (t3 & MK_ST_HAS_OUTPUT) ? o3 : 0;
+        if (p.io_vec && base + 4 <= p.n) {
+            *reinterpret_cast<int4 *>(p.out + base) = make_int4(o0, o1, o2, o3);
+            *reinterpret_cast<uint32_t *>(p.status + base) =
+                (t0 & 0xffu) | (t1 & 0xffu) << 8 | (t2 & 0xffu) << 16 | t3 << 24;
+            if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base) = make_uint4(s0, s1, s2, s3);
+            count_lane(cnt, s0, t0);
+            count_lane(cnt, s1, t1);
+            count_lane(cnt, s2, t2);
+            count_lane(cnt, s3, t3);
+        } else {
+            const int32_t ov[4] = {o0, o1, o2, o3};
+            const uint32_t sv[4] = {s0, s1, s2, s3}, tv[4] = {t0, t1, t2, t3};
+            for (int k = 0; k < 4; ++k) {
+                if (base + k >= p.n) break;
+                p.out[base + k] = ov[k];
+                p.status[base + k] = (uint8_t)tv[k];
+                if (p.steps) p.steps[base + k] = sv[k];
+                count_lane(cnt, sv[k], tv[k]);
+            }
+        }
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+)";
+
+// Kernel of the machine shape.  Thread gid runs inputs gid, gid + lanes, ...
+// one at a time as an MkLane.  Each turn of the wave loop:
+//   1. lanes that ended (MK_SB_DONE) write their result and take their next
+//      input (prefetched one ahead) -- in bulk, once at least `refill` of the
+//      wave's lanes are waiting or nothing else can run;
+//   2. the superblock of the wave's lowest running lane is run for every lane
+//      sitting on it (a scalar switch on a wave-uniform id).
+// A self-loop keeps iterating while enough of its lanes stay in it
+// (MK_LOOP_NEED), so that a few long trips do not hold the whole wave.
+// The policy word `pol` = refill | loop_num << 8 | loop_min << 16: a loop
+// leaves once fewer than loop_num/16 of the lanes it started with remain,
+// for groups of at least loop_min lanes.
+static const char *const kMachineKernel = R"(
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t stride = p.lanes;
+    const uint32_t pol = p.policy;
+    const uint32_t refill_t = pol & 0xffu;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    uint64_t idx = gid;
+    MkLane L;
+    mk_init(L, idx < p.n ? sched_input(p, idx) : 0);
+    if (idx >= p.n) L.sb = MK_SB_IDLE;
+    int32_t nxt = idx + stride < p.n ? sched_input(p, idx + stride) : 0;
+    for (;;) {
+        const bool fin = L.sb == MK_SB_DONE;
+        const unsigned long long finb = __ballot(fin);
+        unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
+        if (finb && (!actb || (uint32_t)__popcll(finb) >= refill_t)) {
+            if (fin) {
+                p.out[idx] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+                p.status[idx] = (uint8_t)L.st;
+                if (p.steps) p.steps[idx] = L.steps;
+                count_lane(cnt, L.steps, L.st);
+                idx += stride;
+                if (idx < p.n) {
+                    mk_init(L, nxt);
+                    nxt = idx + stride < p.n ? sched_input(p, idx + stride) : 0;
+                } else {
+                    L.sb = MK_SB_IDLE;
+                }
+            }
+            actb = __ballot(L.sb < MK_SB_DONE);
+        }
+        if (!actb) {
+            if (!finb) break;
+            continue;
+        }
+        const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
+        if (L.sb == u) mk_run(u, L, p.budget, slots, stride, pol);
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+)";
+
+std::string jit_module_source(const std::string &lane_src, JitShape shape)
 {
     Emitter e;
     // hiprtc declares the fixed-width integer types in __hip_internal only
@@ -273,34 +701,24 @@ std::string jit_module_source(const std::string &lane_src)
     e.line("#define MK_ST_STACK_OVERFLOW %d", MK_ST_STACK_OVERFLOW);
     e.line("#define MK_ST_OUTPUT_STOP %d", MK_ST_OUTPUT_STOP);
     e.line("#define MK_FN static __device__ __forceinline__");
+    // loop policy of the machine shape (see kMachineKernel)
+    e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");
+    e.line("{");
+    e.line("    const uint32_t g0 = (uint32_t)__popcll(__ballot(1));");
+    e.line("    return g0 >= ((pol >> 16) & 0xffu) ? (g0 * ((pol >> 8) & 0xffu) + 15u) / 16u : 0u;");
+    e.line("}");
+    // wave-uniform: some lane of the group is still in the loop, and at least `need`
+    e.line("MK_FN bool mk_keep(bool m, uint32_t need)");
+    e.line("{");
+    e.line("    const uint32_t c = (uint32_t)__popcll(__ballot(m));");
+    e.line("    return c != 0u && c >= need;");
+    e.line("}");
+    e.line("#define MK_LOOP_NEED(pol) mk_loop_need(pol)");
+    e.line("#define MK_KEEP(m, need) mk_keep(m, need)");
     e.s += kDeviceCommon;
     e.s += "\n";
     e.s += lane_src;
-    // One lane per thread per iteration, grid-stride over the batch; the next
-    // input is loaded before the current lane runs, so its HBM latency hides
-    // behind the lane's work.  Counters fold per wave (stats_reduce).
-    e.s += R"(
-extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
-{
-    const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
-    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
-    uint64_t i = gid;
-    int32_t cur = i < p.n ? sched_input(p, i) : 0;
-    for (; i < p.n; i += stride) {
-        const int32_t nxt = i + stride < p.n ? sched_input(p, i + stride) : 0;
-        uint32_t steps, st;
-        const int32_t o = mk_lane(cur, p.budget, slots, p.lanes, &steps, &st);
-        p.out[i] = (st & MK_ST_HAS_OUTPUT) ? o : 0;
-        p.status[i] = (uint8_t)st;
-        if (p.steps) p.steps[i] = steps;
-        count_lane(cnt, steps, st);
-        cur = nxt;
-    }
-    if (p.partials) write_partials(p.partials, gid, cnt);
-}
-)";
+    e.s += shape == JIT_MACHINE ? kMachineKernel : kStreamKernel;
     return e.s;
 }
 

@@ -1,13 +1,18 @@
 // tis_jit.h -- tier 3: a network's compiled schedule (tis_sched.h) turned
-// into straight-line code, one native kernel per (network, stack_cap,
-// stop_on_output), compiled for gfx950 at run time by hiprtc.
+// into native code, one kernel per (network, stack_cap, stop_on_output),
+// compiled for gfx950 at run time by hiprtc.
 //
-// Superblock variants become labels, their micro-ops int64 expressions on
-// local variables (VGPRs instead of the LDS register file of tier 2), exits
-// become gotos (BR), a switch over the clamped operand (JRO), or the lane's
-// result (END / ROUND_END).  Nothing is interpreted at run time: no fetch, no
-// dispatch, no waterfall.  Divergent lanes of a wave are handled by the
-// hardware's exec mask like any other branchy kernel.
+// Superblock variants become code, their micro-ops int64 expressions on
+// VGPR-resident variables (instead of the LDS register file of tier 2).
+// Nothing is interpreted at run time: no fetch, no decode.  Two shapes:
+//   JIT_STREAM  -- acyclic superblock graph (every lane runs a bounded
+//                  straight-line path): labels + gotos in one lane function;
+//                  the kernel streams 4 lanes per thread with vector I/O.
+//   JIT_MACHINE -- cyclic graph (data-dependent loops): the lane is a
+//                  resumable state machine (MkLane + mk_run per variant, self
+//                  loops as rotated do-while loops); the kernel dispatches one
+//                  superblock per wave turn and refills finished lanes with
+//                  new inputs while the rest of the wave keeps running.
 #pragma once
 
 #include <cstdint>
@@ -21,21 +26,34 @@ struct JitLimits {
     uint32_t max_variants = 4096; // superblock variants (labels)
     size_t max_dops = 4096;       // micro-ops in the reachable code (hiprtc time grows
                                   // superlinearly: 14K straight-line ops take ~150 s)
+    bool force_machine = false;   // machine shape even for acyclic graphs (tests)
 };
 
-// The lane function for `p` in portable C++ (host g++ or HIP device):
+enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
+
+// The lane source for `p` in portable C++ (host g++ or HIP device).  Both
+// shapes define
 //   MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *slots,
 //                         uint64_t sstride, uint32_t *steps, uint32_t *status)
-// `slots` points at stack slot 0 of the lane, slot s at slots[s * sstride].
-// MK_FN is defined by the includer.  Returns false (why) when over limits.
-bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why);
+// (the machine shape builds it from mk_init/mk_run, driving MK_LOOP_NEED /
+// MK_KEEP which the includer defines).  `slots` points at stack slot 0 of the
+// lane, slot s at slots[s * sstride].  MK_FN is defined by the includer.
+// Returns false (why) when over limits.
+bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why,
+                     JitShape *shape = nullptr);
 
 // Full hiprtc translation unit: prelude, shared device code
-// (mk_device_common.inc), the lane function and the kernel `mk_jit_exec`.
-std::string jit_module_source(const std::string &lane_src);
+// (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of
+// the given shape.
+std::string jit_module_source(const std::string &lane_src, JitShape shape);
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
+constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
+
+// Default machine-shape policy word (kMachineKernel): refill once 8 lanes of
+// the wave wait; a loop of >= 16 lanes leaves when fewer than 12/16 remain.
+constexpr uint32_t kJitPolicy = 8u | (12u << 8) | (16u << 16);
 
 } // namespace mk

@@ -25,7 +25,8 @@ def lib():
         h.mkc_free.argtypes = [C.c_void_p]
         h.mkc_emulate.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
-        h.mkc_jit_lane.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_char_p, C.c_size_t]
+        h.mkc_jit_lane.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         _lib = h
     return _lib
 
@@ -49,17 +50,24 @@ def _load(nodes):
     return h, keep
 
 
-def jit_lane(nodes, *, stack_cap=None, stop_on_output=False):
-    """(source of the native tier's lane function, stack slots per lane)."""
+SHAPES = {0: "stream", 1: "machine"}
+
+
+def jit_lane(nodes, *, stack_cap=None, stop_on_output=False, machine=False, with_shape=False):
+    """(source of the native tier's lane code, stack slots per lane[, shape]).
+    ``machine``: force the machine shape (resumable lane) on acyclic networks too."""
     h, _keep = _load(nodes)
     try:
         ns = C.c_uint32()
+        sh = C.c_int()
         buf = C.create_string_buffer(1 << 24)
         rc = lib().mkc_jit_lane(h, 1024 if stack_cap is None else stack_cap, 1 if stop_on_output else 0,
-                                C.byref(ns), buf, len(buf))
+                                1 if machine else 0, C.byref(ns), C.byref(sh), buf, len(buf))
         if rc == 1:
             raise NotCompiled(buf.value.decode())
         assert rc == 0, rc
+        if with_shape:
+            return buf.value.decode(), ns.value, SHAPES[sh.value]
         return buf.value.decode(), ns.value
     finally:
         lib().mkc_free(h)

@@ -255,3 +255,28 @@ def test_wide_immediates_on_symbolic_acc(gpu, mode):
     nodes = [("n", "program", prog)]
     xs = po.gen_inputs(SEED, 4096)
     assert_same(mk.Network(nodes).compute_batch(xs, mode=_m(mode)), oracle(nodes, xs), "wide imm")
+
+
+# The native tier's two kernel shapes (tis_jit.h): acyclic schedules stream,
+# cyclic ones run as per-lane state machines with refill.  Force the machine
+# shape on every network (MK_JIT_SHAPE is read when a network's kernel is
+# generated) and vary its wave policy (MK_JIT_POLICY, read per launch).
+@pytest.mark.parametrize("policy", ["8,12,16", "1,0,64", "64,16,1", "16,8,4"])
+def test_machine_shape_and_policies(gpu, monkeypatch, policy):
+    monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+    monkeypatch.setenv("MK_JIT_POLICY", policy)
+    cases = [("c2", mk.networks.example_network(), po.gen_inputs(SEED, 5000), {}),
+             ("c3", mk.networks.sample_network(), po.gen_inputs(SEED, 5000), {}),
+             ("c5", mk.networks.countdown_network(), po.gen_inputs(SEED, 5000, kind=1, mask=1023), {}),
+             ("c5b", mk.networks.countdown_network(), po.gen_inputs(SEED, 3000, kind=1, mask=1023), {"budget": 700})]
+    for seed in range(0, 240, 7):
+        kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=[1, 3, 8, 16, 17, 40, 1024][seed % 7],
+                  stop_on_output=(seed % 5 == 4))
+        cases.append((f"seed{seed}", random_network(seed), po.gen_inputs(seed * 7919 + 1, 777), kw))
+    for label, nodes, xs, kw in cases:
+        net = mk.Network(nodes)
+        got = net.compute_batch(xs, **kw)
+        plan = net.plan(stack_cap=kw.get("stack_cap"), stop_on_output=kw.get("stop_on_output", False))
+        if label.startswith("c"):
+            assert "shape=machine" in plan, plan
+        assert_same(got, oracle(nodes, xs, **kw), f"{label} policy {policy}")

@@ -24,6 +24,8 @@ HEADER = """#include <cstdint>
 #include <cstddef>
 #include <vector>
 #define MK_FN static inline
+#define MK_LOOP_NEED(pol) 0u
+#define MK_KEEP(m, need) (m)
 """
 
 
@@ -59,12 +61,14 @@ def run_lane(lib, i, xs, budget):
     return out, st, sp
 
 
-def check_cases(tmp_path, cases):
-    """cases: [(label, nodes, xs, kw)] -- every case compiled and compared."""
+def check_cases(tmp_path, cases, machine=False):
+    """cases: [(label, nodes, xs, kw)] -- every case compiled and compared.
+    ``machine``: the resumable (machine-shape) lane for every case."""
     srcs, keep = [], []
     for label, nodes, xs, kw in cases:
         try:
-            src, ns = sc.jit_lane(nodes, stack_cap=kw.get("stack_cap"), stop_on_output=kw.get("stop_on_output", False))
+            src, ns = sc.jit_lane(nodes, stack_cap=kw.get("stack_cap"), stop_on_output=kw.get("stop_on_output", False),
+                                  machine=machine)
         except sc.NotCompiled:
             continue  # tier 1 handles it; covered elsewhere
         srcs.append((src, ns))
@@ -79,7 +83,8 @@ def check_cases(tmp_path, cases):
     return [k[0] for k in keep]
 
 
-def test_configs(tmp_path):
+@pytest.mark.parametrize("machine", [False, True])
+def test_configs(tmp_path, machine):
     cases = []
     for name in sorted(mk.networks.CONFIGS):
         kind = 1 if name.startswith("c5") else 0
@@ -90,12 +95,13 @@ def test_configs(tmp_path):
         cases.append((f"c2_budget{b}", mk.networks.example_network(), po.gen_inputs(SEED, 300), {"budget": b}))
         cases.append((f"c5_budget{b}", mk.networks.countdown_network(),
                       po.gen_inputs(SEED, 300, kind=1, mask=1023), {"budget": b * 37}))
-    done = check_cases(tmp_path, cases)
+    done = check_cases(tmp_path, cases, machine)
     # the deep pipelines exceed the native tier's size limit (tier 2 runs them)
     assert set(c[0] for c in cases) - set(done) == {"c4_pipeline", "c4_d1024"}
 
 
-def test_wide_immediates_and_stop(tmp_path):
+@pytest.mark.parametrize("machine", [False, True])
+def test_wide_immediates_and_stop(tmp_path, machine):
     prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
             "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
             "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
@@ -103,17 +109,26 @@ def test_wide_immediates_and_stop(tmp_path):
     cases = [("wide", [("n", "program", prog)], po.gen_inputs(SEED, 2048), {}),
              ("budget", loop, [0] * 8, {"budget": 11}),
              ("stop", loop, [0] * 8, {"stop_on_output": True})]
-    assert len(check_cases(tmp_path, cases)) == 3
+    assert len(check_cases(tmp_path, cases, machine)) == 3
 
 
+@pytest.mark.parametrize("machine", [False, True])
 @pytest.mark.parametrize("block", range(4))
-def test_random_networks(tmp_path, block):
+def test_random_networks(tmp_path, block, machine):
     cases = []
     for seed in range(block * 40, block * 40 + 40):
         kw = dict(budget=[37, 200, 1000][seed % 3], stack_cap=[1, 3, 8, 16, 17, 40, 1024][seed % 7],
                   stop_on_output=(seed % 5 == 4))
         cases.append((f"seed{seed}", random_network(seed), po.gen_inputs(seed * 7919 + 1, 256), kw))
-    assert len(check_cases(tmp_path, cases)) >= 30
+    assert len(check_cases(tmp_path, cases, machine)) >= 30
+
+
+def test_shapes():
+    # acyclic schedules stream; data-dependent loops get the machine shape
+    assert sc.jit_lane(mk.networks.example_network(), with_shape=True)[2] == "stream"
+    assert sc.jit_lane(mk.networks.sample_network(), with_shape=True)[2] == "stream"
+    src, _, shape = sc.jit_lane(mk.networks.countdown_network(), with_shape=True)
+    assert shape == "machine" and "do {" in src
 
 
 def test_module_compiles_for_gfx950():
