@@ -81,6 +81,17 @@ def cpu_baseline(nodes, gen_kind, mask, seconds=10.0):
     }
 
 
+def measured_traffic(workload):
+    """HBM bytes per executor launch from the committed rocprofv3 PMC pass
+    for this workload (profiles/pmc_<workload>.json, written by
+    tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
 def valu_peak(stream):
     """Live dependency-free v_add_u32 probe on this GPU (lane-ops/s)."""
     blocks, iters = 256 * 8 * 4, 2000
@@ -146,24 +157,30 @@ def main():
     st = torch.empty(lanes, dtype=torch.uint8, device="cuda")
     stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
 
-    def step(stats_ptr):
-        net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats_ptr,
+    def step(count):
+        # count: the launch adds its counters on the device (folded once, below)
+        net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=None,
                            in_ptr=None if args.gen_inputs else x.data_ptr(), in_kind=N.MK_IN_I32, seed=SEED,
-                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, mode=args.mode)
+                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, mode=args.mode,
+                           defer_stats=count)
 
     net.prepare(mode=args.mode, device=dev)  # schedule + native kernel compiled before any timing
     for _ in range(args.warmup):
-        step(None)
+        step(False)
+    net.stats_fold(stats.data_ptr(), device=dev, stream=sh)  # clear anything left on the device
     torch.cuda.synchronize()
     stats.zero_()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # Timed region: K executor launches, each counting its lanes' retired
+    # instructions on the device, plus the one fold of those counters.
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(args.steps):
-        step(stats.data_ptr())
+        step(True)
+    net.stats_fold(stats.data_ptr(), device=dev, stream=sh)
     e1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -171,12 +188,22 @@ def main():
     wall = time.perf_counter() - t0
     kernel_s = e0.elapsed_time(e1) * 1e-3  # HIP events on the launch stream
 
+    # Average duration of one executor launch (the dominant kernel) for the
+    # roofline: HIP events around K launches on the launch stream.
+    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k0.record(stream)
+    for _ in range(args.steps):
+        step(False)
+    k1.record(stream)
+    torch.cuda.synchronize()
+    launch_s = k0.elapsed_time(k1) * 1e-3 / args.steps
+
     # per-rank -> whole job (max time over ranks, summed work)
-    t = torch.tensor([wall, kernel_s], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall, kernel_s, launch_s], dtype=torch.float64, device="cuda")
     tot = mk.dist.reduce_counters(stats.clone(), dist)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kern_max = t.tolist()
+    wall_max, kern_max, launch_max = t.tolist()
     tot = tot.cpu().numpy()
     retired, with_out, finished = int(tot[0]), int(tot[1]), int(tot[2])
     assert finished == lanes * world * args.steps, (finished, lanes, world, args.steps)
@@ -200,9 +227,39 @@ def main():
         except Exception as e:  # pragma: no cover
             log("valu probe failed:", e)
     peak = max(SPEC_LANE_OPS, peak_meas or 0.0)
-    achieved = K_LANE_OPS * per_gpu_kernel_rate
+    # per launch of the executor kernel: algorithmic lane-ops and bytes
+    instr_per_launch = retired / world / args.steps
+    achieved = K_LANE_OPS * instr_per_launch / launch_max
     bytes_per_lane = (0 if args.gen_inputs else 4) + 4 + 1  # int32 input read, int32 out + u8 status written
-    hbm_achieved = bytes_per_lane * lanes * args.steps / kern_max
+    bytes_per_launch = bytes_per_lane * lanes
+    hbm_achieved = bytes_per_launch / launch_max
+    traffic = measured_traffic(name)
+    hbm = {
+        "bound": "hbm",
+        "achieved": hbm_achieved / 1e9,
+        "peak": HBM_PEAK / 1e9,
+        "unit": "GB/s",
+        "frac": hbm_achieved / HBM_PEAK,
+        "traffic": traffic,
+        "bytes_per_lane": bytes_per_lane,
+        "bytes_per_launch": bytes_per_launch,
+        "launch_us": launch_max * 1e6,
+    }
+    issue = {
+        "bound": "valu",
+        "achieved": achieved / 1e12,
+        "peak": peak / 1e12,
+        "unit": "Tlane-op/s",
+        "frac": achieved / peak,
+        "traffic": traffic,
+        "k_lane_ops_per_instr": K_LANE_OPS,
+        "peak_spec": SPEC_LANE_OPS / 1e12,
+        "peak_measured": None if peak_meas is None else peak_meas / 1e12,
+        "launch_us": launch_max * 1e6,
+    }
+    # The dominant kernel's roofline is the tighter of the two bounds: the
+    # byte stream for short networks (C2, C3), integer issue for long ones.
+    hbm_bound = hbm_achieved / HBM_PEAK >= achieved / peak
 
     if rank == 0:
         cpu = None
@@ -232,25 +289,9 @@ def main():
             "results_per_s": with_out / wall_max,
             "node_instr_per_lane": retired / (lanes * world * args.steps),
             "kernel_ms_per_step": kern_max / args.steps * 1e3,
-            "roofline": {
-                "bound": "valu",
-                "achieved": achieved / 1e12,
-                "peak": peak / 1e12,
-                "unit": "Tlane-op/s",
-                "frac": achieved / peak,
-                "traffic": None,
-                "k_lane_ops_per_instr": K_LANE_OPS,
-                "peak_spec": SPEC_LANE_OPS / 1e12,
-                "peak_measured": None if peak_meas is None else peak_meas / 1e12,
-            },
-            "roofline_hbm": {
-                "bound": "hbm",
-                "achieved": hbm_achieved / 1e9,
-                "peak": HBM_PEAK / 1e9,
-                "unit": "GB/s",
-                "frac": hbm_achieved / HBM_PEAK,
-                "bytes_per_lane": bytes_per_lane,
-            },
+            "roofline": hbm if hbm_bound else issue,
+            "roofline_issue": issue,
+            "roofline_hbm": hbm,
             "cpu_baseline": cpu,
         }
         if gather_ms is not None:

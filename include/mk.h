@@ -80,6 +80,12 @@ typedef struct {
  * select the tier-2 superblock interpreter, MK_FLAG_FORCE_INTERP tier 1.
  * MK_JIT=0 in the environment disables tier 3. */
 #define MK_FLAG_JIT 16u
+/* Device API: gather the counters of this launch without folding them into
+ * d_stats yet (d_stats may be NULL).  Counters of deferred launches on one
+ * handle and device accumulate on the device until mk_stats_fold (or the
+ * next launch that folds); launches that defer must be stream-ordered with
+ * each other and with the fold. */
+#define MK_FLAG_DEFER_STATS 32u
 
 typedef struct {
     uint32_t budget;      /* retired node-instructions per lane; 0 = 1<<20          */
@@ -138,6 +144,11 @@ typedef struct {
 int mk_compute_device(mk_net *net, int device, const mk_input *in, size_t n, int32_t *d_out,
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats,
                       const mk_opts *opts, void *stream);
+
+/* Add the counters accumulated by MK_FLAG_DEFER_STATS launches on `device`
+ * into d_stats (device uint64[MK_STATS_LEN]) and clear them; asynchronous
+ * on `stream`.  Replaces nothing in the reference (it has no counters). */
+int mk_stats_fold(mk_net *net, int device, uint64_t *d_stats, void *stream);
 
 /* Fill d_out[i] = gen(seed, offset + i) on device (same generator as MK_IN_GEN). */
 int mk_generate_inputs_device(int device, uint64_t seed, uint32_t gen_kind, uint32_t gen_mask,

@@ -37,6 +37,7 @@ MK_FLAG_FORCE_INTERP = 2
 MK_FLAG_TILE = 4
 MK_FLAG_REFILL = 8
 MK_FLAG_JIT = 16
+MK_FLAG_DEFER_STATS = 32
 
 MK_IN_I64 = 0
 MK_IN_I32 = 1
@@ -101,6 +102,7 @@ SIGNATURES = {
             C.c_void_p,
         ],
     ),
+    "mk_stats_fold": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "mk_generate_inputs_device": (
         C.c_int,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p, C.c_void_p],

@@ -84,15 +84,19 @@ __device__ __forceinline__ int32_t lane_input(const KParams &p, uint64_t i)
 }
 
 
-// Folds the per-wave partials into the caller's counters: one thread per
-// wave partial, a block tree in LDS, then one atomic per counter per block.
-__global__ void __launch_bounds__(256) stats_reduce(const unsigned long long *__restrict__ partials,
-                                                    uint32_t nwaves, unsigned long long *stats)
+// Folds the per-wave partial rows into the caller's counters and clears
+// them: one thread per row, a block tree in LDS, then one atomic per counter
+// per block.  Rows accumulate across launches until folded (deferred stats).
+__global__ void __launch_bounds__(256) stats_reduce(unsigned long long *__restrict__ partials, uint32_t nwaves,
+                                                    unsigned long long *stats)
 {
     __shared__ unsigned long long acc[8][256];
     const uint32_t t = threadIdx.x, w = blockIdx.x * 256 + t;
 #pragma unroll
-    for (int k = 0; k < 8; k++) acc[k][t] = w < nwaves ? partials[(size_t)w * 8 + k] : 0ull;
+    for (int k = 0; k < 8; k++) {
+        acc[k][t] = w < nwaves ? partials[(size_t)w * 8 + k] : 0ull;
+        if (w < nwaves) partials[(size_t)w * 8 + k] = 0ull;
+    }
     __syncthreads();
     for (uint32_t h = 128; h > 0; h >>= 1) {
         if (t < h) {
@@ -1047,28 +1051,34 @@ int ensure_sched_device(SchedCache *sc, int d)
 }
 
 // Caller holds h->mu.  Per-wave counter buffer for `lanes` resident lanes.
+// The per-wave counter rows are allocated once per device context for the
+// largest resident grid (2048 threads per CU) and zeroed; kernels add into
+// them and stats_reduce folds and clears them, so counts of launches that
+// defer their stats (MK_FLAG_DEFER_STATS) accumulate until the next fold.
 int ensure_partials(DevCtx &c, uint64_t lanes)
 {
-    const size_t need = (size_t)((lanes + 63) / 64) * 8 * sizeof(unsigned long long);
-    if (need <= c.partials_bytes) return MK_OK;
-    if (c.d_partials) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(c.d_partials);
-        c.d_partials = nullptr;
-        c.partials_bytes = 0;
+    if (!c.d_partials) {
+        const size_t rows = (size_t)std::max(c.cus, 1) * 32;
+        const size_t bytes = rows * 8 * sizeof(unsigned long long);
+        if (hipMalloc(&c.d_partials, bytes) != hipSuccess) return MK_ENOMEM;
+        if (hipMemset(c.d_partials, 0, bytes) != hipSuccess) return MK_EDEVICE;
+        c.partials_bytes = bytes;
     }
-    if (hipMalloc(&c.d_partials, need) != hipSuccess) return MK_ENOMEM;
-    c.partials_bytes = need;
-    return MK_OK;
+    return (lanes + 63) / 64 <= c.partials_bytes / 64 ? MK_OK : MK_ELIMIT; // one 64-byte row per wave
 }
 
-int launch_stats_reduce(DevCtx &c, uint64_t lanes, uint64_t *d_stats, hipStream_t stream)
+int launch_stats_reduce(DevCtx &c, uint64_t *d_stats, hipStream_t stream)
 {
-    const uint32_t nwaves = (uint32_t)((lanes + 63) / 64);
-    hipLaunchKernelGGL(stats_reduce, dim3((nwaves + 255) / 256), dim3(256), 0, stream,
-                       (const unsigned long long *)c.d_partials, nwaves, reinterpret_cast<unsigned long long *>(d_stats));
+    const uint32_t nrows = (uint32_t)(c.partials_bytes / 64);
+    hipLaunchKernelGGL(stats_reduce, dim3((nrows + 255) / 256), dim3(256), 0, stream, c.d_partials, nrows,
+                       reinterpret_cast<unsigned long long *>(d_stats));
     return hipGetLastError() == hipSuccess ? MK_OK : MK_EDEVICE;
 }
+
+// Counters are gathered when the caller passes stats or defers them; folded
+// into d_stats right after the launch unless deferred.
+bool counting(const uint64_t *d_stats, uint32_t flags) { return d_stats || (flags & MK_FLAG_DEFER_STATS); }
+bool fold_now(const uint64_t *d_stats, uint32_t flags) { return d_stats && !(flags & MK_FLAG_DEFER_STATS); }
 
 // Caller holds h->mu.  Tier-2 launch; asynchronous on `stream`.
 int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
@@ -1121,8 +1131,8 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
-    p.partials = d_stats ? c.d_partials : nullptr;
+    if (counting(d_stats, flags) && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
     p.slots = sd.d_slots;
     p.lanes = lanes;
     p.vlanes = vlanes;
@@ -1136,7 +1146,7 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     const uint32_t *entry = sd.d_entry, *jtab = sd.d_jtab;
     void *args[] = {(void *)&code, (void *)&entry, (void *)&jtab, (void *)&p};
     if (hipLaunchKernel(fn, dim3(blocks), dim3(B), args, lds, stream) != hipSuccess) return MK_EDEVICE;
-    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
+    return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
 
 // ---- tier 3: native kernel per schedule (tis_jit.h) ------------------------
@@ -1160,8 +1170,9 @@ bool jit_compile(SchedCache *sc)
     const auto t0 = std::chrono::steady_clock::now();
     std::string lane;
     JitLimits lim;
-    const char *shp = std::getenv("MK_JIT_SHAPE"); // "machine": force the machine shape (experiments)
+    const char *shp = std::getenv("MK_JIT_SHAPE"); // "machine" / "stream": force a shape (experiments)
     lim.force_machine = shp && std::strcmp(shp, "machine") == 0;
+    lim.force_stream = shp && std::strcmp(shp, "stream") == 0;
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape)) return false;
     const std::string src = jit_module_source(lane, J.shape);
     J.src_bytes = src.size();
@@ -1222,7 +1233,8 @@ uint32_t jit_policy()
 
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
 int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
-                      uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, hipStream_t stream)
+                      uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, uint32_t flags,
+                      hipStream_t stream)
 {
     int rc = ensure_jit_device(sc, d);
     if (rc) return rc;
@@ -1261,8 +1273,8 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
-    p.partials = d_stats ? c.d_partials : nullptr;
+    if (counting(d_stats, flags) && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
     p.slots = P.nslots ? sd.d_slots : nullptr;
     p.lanes = lanes;
     p.vlanes = lanes;
@@ -1273,7 +1285,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     void *args[] = {(void *)&p};
     if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, kJitBlock, 1, 1, 0, stream, args, nullptr) != hipSuccess)
         return MK_EDEVICE;
-    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
+    return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
 
 enum Tier { TIER_NONE, TIER_INTERP, TIER_COMPILED, TIER_NATIVE };
@@ -1306,7 +1318,8 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     resolve_opts(o, budget, cap, flags);
     SchedCache *sc = nullptr;
     switch (pick_tier(h, cap, flags, &sc)) {
-    case TIER_NATIVE: return launch_jit_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, stream);
+    case TIER_NATIVE:
+        return launch_jit_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, flags, stream);
     case TIER_COMPILED:
         return launch_sched_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, flags, stream);
     case TIER_NONE: return MK_ELIMIT; // native tier demanded but unavailable (mk_net_plan says why)
@@ -1347,8 +1360,8 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    if (d_stats && (rc = ensure_partials(c, lanes))) return rc;
-    p.partials = d_stats ? c.d_partials : nullptr;
+    if (counting(d_stats, flags) && (rc = ensure_partials(c, lanes))) return rc;
+    p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
     p.budget = budget;
     p.stack_cap = cap;
     p.flags = flags;
@@ -1360,7 +1373,7 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     void *args[] = {(void *)&code, (void *)&p};
     if (hipLaunchKernel(L.fn, dim3(L.blocks), dim3(kBlock), args, L.lds, stream) != hipSuccess)
         return MK_EDEVICE;
-    return d_stats ? launch_stats_reduce(c, lanes, d_stats, stream) : MK_OK;
+    return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
 
 void set_err(char *err, size_t len, const std::string &s)
@@ -1494,6 +1507,21 @@ int mk_compute_device(mk_net *h, int device, const mk_input *in, size_t n, int32
     if (device < 0 || device >= ndev || device >= mk::kMaxDevices) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     return mk::launch_locked(h, device, in, n, d_out, d_status, d_steps, d_stats, opts, (hipStream_t)stream);
+}
+
+int mk_stats_fold(mk_net *h, int device, uint64_t *d_stats, void *stream)
+{
+    if (!h || !d_stats) return MK_EINVAL;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev || device >= mk::kMaxDevices) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = mk::ensure_device(h, device);
+    if (rc) return rc;
+    mk::DevCtx &c = h->dev[device];
+    mk::DeviceGuard g(device);
+    if ((rc = mk::ensure_partials(c, 0))) return rc;
+    return mk::launch_stats_reduce(c, d_stats, (hipStream_t)stream);
 }
 
 int mk_generate_inputs_device(int device, uint64_t seed, uint32_t gen_kind, uint32_t gen_mask, uint64_t offset,

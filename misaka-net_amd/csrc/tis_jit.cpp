@@ -545,7 +545,7 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     Graph g;
     if (!analyze(p, lim, g, why)) return false;
     Emitter e;
-    const JitShape s = lim.force_machine || g.cyclic ? JIT_MACHINE : JIT_STREAM;
+    const JitShape s = lim.force_stream ? JIT_STREAM : (lim.force_machine || g.cyclic) ? JIT_MACHINE : JIT_STREAM;
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else

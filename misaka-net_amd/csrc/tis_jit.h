@@ -27,6 +27,7 @@ struct JitLimits {
     size_t max_dops = 4096;       // micro-ops in the reachable code (hiprtc time grows
                                   // superlinearly: 14K straight-line ops take ~150 s)
     bool force_machine = false;   // machine shape even for acyclic graphs (tests)
+    bool force_stream = false;    // stream shape even for cyclic graphs (experiments)
 };
 
 enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
@@ -52,8 +53,11 @@ constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
 
-// Default machine-shape policy word (kMachineKernel): refill once 8 lanes of
-// the wave wait; a loop of >= 16 lanes leaves when fewer than 12/16 remain.
-constexpr uint32_t kJitPolicy = 8u | (12u << 8) | (16u << 16);
+// Default machine-shape policy word (kMachineKernel): generations -- a wave
+// refills only once all its lanes have ended and loops never leave early.
+// Measured on MI355X (C5): ahead of every early-refill / early-leave setting
+// tried (refill 1..48 lanes, leave at 8..14/16), whose extra dispatches and
+// small groups cost more than the idle lanes they save.
+constexpr uint32_t kJitPolicy = 64u | (0u << 8) | (64u << 16);
 
 } // namespace mk

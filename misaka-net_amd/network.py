@@ -204,10 +204,12 @@ class Network:
 
     def compute_device(self, n, *, out_ptr, status_ptr, steps_ptr=None, stats_ptr=None, device=0, stream=None,
                        in_ptr=None, in_kind=N.MK_IN_I32, seed=0, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0,
-                       budget=None, stack_cap=None, stop_on_output=False, interp=False, mode=None):
+                       budget=None, stack_cap=None, stop_on_output=False, interp=False, mode=None,
+                       defer_stats=False):
         """Launch on device memory (raw pointers, e.g. torch ``data_ptr()``);
         asynchronous on ``stream`` (a HIP stream handle, e.g.
-        ``torch.cuda.current_stream().cuda_stream``)."""
+        ``torch.cuda.current_stream().cuda_stream``).  ``defer_stats``: keep
+        this launch's counters on the device until :meth:`stats_fold`."""
         mi = N.mk_input()
         mi.kind = N.MK_IN_GEN if in_ptr is None else in_kind
         mi.data = in_ptr
@@ -216,10 +218,17 @@ class Network:
         mi.gen_mask = gen_mask
         mi.offset = offset
         o = make_opts(budget, stack_cap, stop_on_output, None, interp, mode)
+        if defer_stats:
+            o.flags |= N.MK_FLAG_DEFER_STATS
         rc = N.lib().mk_compute_device(
             self._h, device, C.byref(mi), n, out_ptr, status_ptr, steps_ptr, stats_ptr, C.byref(o), stream
         )
         N.check(rc, "mk_compute_device")
+
+    def stats_fold(self, stats_ptr, *, device=0, stream=None):
+        """Add the counters of deferred launches on ``device`` into the
+        device uint64[MK_STATS_LEN] at ``stats_ptr`` (asynchronous)."""
+        N.check(N.lib().mk_stats_fold(self._h, device, stats_ptr, stream), "mk_stats_fold")
 
 
 def generate_inputs_device(n, out_ptr, *, seed, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0, device=0, stream=None):

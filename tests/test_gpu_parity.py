@@ -280,3 +280,30 @@ def test_machine_shape_and_policies(gpu, monkeypatch, policy):
         if label.startswith("c"):
             assert "shape=machine" in plan, plan
         assert_same(got, oracle(nodes, xs, **kw), f"{label} policy {policy}")
+
+
+# Deferred counters (MK_FLAG_DEFER_STATS + mk_stats_fold) add up to the same
+# totals as per-launch folding, and to the oracle's, on every tier.
+@pytest.mark.parametrize("mode", ["auto", "tile", "interp"])
+def test_deferred_stats_fold(gpu, mode):
+    import torch
+
+    nodes = mk.networks.countdown_network()
+    net = mk.Network(nodes)
+    n = 5000
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s_imm = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+    s_def = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    kw = dict(out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), gen_kind=N.MK_GEN_MASKED, gen_mask=1023,
+              stream=sh, mode=_m(mode))
+    for seed in (1, 2, 3):
+        net.compute_device(n, stats_ptr=s_imm.data_ptr(), seed=seed, **kw)
+    for seed in (1, 2, 3):
+        net.compute_device(n, stats_ptr=None, seed=seed, defer_stats=True, **kw)
+    net.stats_fold(s_def.data_ptr(), stream=sh)
+    torch.cuda.synchronize()
+    assert s_imm.tolist() == s_def.tolist()
+    steps = sum(int(oracle(nodes, po.gen_inputs(seed, n, kind=1, mask=1023))[2].sum()) for seed in (1, 2, 3))
+    assert s_def[0].item() == steps and s_def[2].item() == 3 * n

@@ -5,6 +5,6 @@ import sys
 label = sys.argv[1] if len(sys.argv) > 1 else ""
 for line in sys.stdin:
     r = json.loads(line)
-    print(f"{label[:70]:70s} {r['value']/1e9:9.1f} G/s kern {r['kernel_ms_per_step']*1e3:8.1f}us "
-          f"issue {r['roofline']['frac']:.3f} hbm {r['roofline_hbm']['frac']:.3f} "
+    print(f"{label[:70]:70s} {r['value']/1e9:9.1f} G/s launch {r['roofline']['launch_us']:8.1f}us "
+          f"issue {r['roofline_issue']['frac']:.3f} hbm {r['roofline_hbm']['frac']:.3f} "
           f"{r['config'].get('executor','')[:60]}")
