@@ -118,6 +118,7 @@ def main():
                     help="force an executor mode (default: automatic)")
     ap.add_argument("--gen-inputs", action="store_true",
                     help="diagnostic: generate inputs inside the executor instead of reading them from HBM")
+    ap.add_argument("--graph", action="store_true", help="replay the timed launches as one captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -157,12 +158,17 @@ def main():
     st = torch.empty(lanes, dtype=torch.uint8, device="cuda")
     stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
 
-    def step(count):
-        # count: the launch adds its counters on the device (folded once, below)
-        net.compute_device(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=None,
-                           in_ptr=None if args.gen_inputs else x.data_ptr(), in_kind=N.MK_IN_I32, seed=SEED,
-                           gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev, stream=sh, mode=args.mode,
-                           defer_stats=count)
+    # count: the launch adds its counters on the device (folded once, below)
+    launchers = {
+        count: net.device_launcher(lanes, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(),
+                                   in_ptr=None if args.gen_inputs else x.data_ptr(), in_kind=N.MK_IN_I32,
+                                   seed=SEED, gen_kind=gen_kind, gen_mask=mask, offset=lo, device=dev,
+                                   mode=args.mode, defer_stats=count)
+        for count in (False, True)
+    }
+
+    def step(count, stream_handle=sh):
+        launchers[count](stream_handle)
 
     net.prepare(mode=args.mode, device=dev)  # schedule + native kernel compiled before any timing
     for _ in range(args.warmup):
@@ -175,13 +181,29 @@ def main():
     torch.cuda.synchronize()
     # Timed region: K executor launches, each counting its lanes' retired
     # instructions on the device, plus the one fold of those counters.
+    graph = None
+    if args.graph:
+        # the K launches + fold captured once as a HIP graph and replayed below
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ch = torch.cuda.current_stream().cuda_stream
+            for _ in range(args.steps):
+                step(True, ch)
+            net.stats_fold(stats.data_ptr(), device=dev, stream=ch)
+        torch.cuda.synchronize()
+        stats.zero_()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.steps):
-        step(True)
-    net.stats_fold(stats.data_ptr(), device=dev, stream=sh)
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            step(True)
+        net.stats_fold(stats.data_ptr(), device=dev, stream=sh)
     e1.record(stream)
+    enqueue_s = time.perf_counter() - t0  # host time to issue the timed work
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -289,6 +311,8 @@ def main():
             "results_per_s": with_out / wall_max,
             "node_instr_per_lane": retired / (lanes * world * args.steps),
             "kernel_ms_per_step": kern_max / args.steps * 1e3,
+            "host_enqueue_us_per_step": enqueue_s / args.steps * 1e6,
+            "launch": "hip graph replay" if args.graph else "stream launches",
             "roofline": hbm if hbm_bound else issue,
             "roofline_issue": issue,
             "roofline_hbm": hbm,

@@ -225,6 +225,31 @@ class Network:
         )
         N.check(rc, "mk_compute_device")
 
+    def device_launcher(self, n, *, out_ptr, status_ptr, steps_ptr=None, device=0, in_ptr=None,
+                        in_kind=N.MK_IN_I32, seed=0, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0, budget=None,
+                        stack_cap=None, stop_on_output=False, mode=None, defer_stats=False):
+        """``compute_device`` with every argument fixed: returns ``launch(stream)``
+        whose host cost is one foreign call (the ctypes structs are built once)."""
+        mi = N.mk_input()
+        mi.kind = N.MK_IN_GEN if in_ptr is None else in_kind
+        mi.data = in_ptr
+        mi.seed = seed
+        mi.gen_kind = gen_kind
+        mi.gen_mask = gen_mask
+        mi.offset = offset
+        o = make_opts(budget, stack_cap, stop_on_output, None, False, mode)
+        if defer_stats:
+            o.flags |= N.MK_FLAG_DEFER_STATS
+        fn, h, pmi, po = N.lib().mk_compute_device, self._h, C.byref(mi), C.byref(o)
+
+        def launch(stream=None):
+            rc = fn(h, device, pmi, n, out_ptr, status_ptr, steps_ptr, None, po, stream)
+            if rc:
+                N.check(rc, "mk_compute_device")
+
+        launch.keep = (mi, o, self)
+        return launch
+
     def stats_fold(self, stats_ptr, *, device=0, stream=None):
         """Add the counters of deferred launches on ``device`` into the
         device uint64[MK_STATS_LEN] at ``stats_ptr`` (asynchronous)."""
