@@ -225,7 +225,8 @@ class MasterNode:
                                              devices=self.devices, steps=False)
         if not (int(r.status[0]) & N.MK_ST_HAS_OUTPUT):
             return http_error("network produced no output", 504)
-        return Response(200, json.dumps({"value": int(r.out[0])}) + "\n", "application/json")
+        # json.NewEncoder(w).Encode(clientOutResponse{...}) (master.go:219): compact, newline-terminated
+        return Response(200, json.dumps({"value": int(r.out[0])}, separators=(",", ":")) + "\n", "application/json")
 
     def _compute_batch(self, query, body, ctype):
         if not self.is_running:

@@ -110,9 +110,10 @@ def post(port, path, body="", ctype=FORM):
 @pytest.mark.gpu
 def test_http_compute_example(server):
     assert post(server, "/run") == (200, "text/plain; charset=utf-8", "Success")
-    assert post(server, "/compute", "value=5") == (200, "application/json", '{"value": 7}\n')
-    assert post(server, "/compute", "value=4294967301")[2] == '{"value": 7}\n'  # int32(v), master.go:237
-    assert post(server, "/compute", "value=2147483647")[2] == '{"value": -2147483647}\n'
+    # Go's json.Encoder: compact, newline-terminated (master.go:219)
+    assert post(server, "/compute", "value=5") == (200, "application/json", '{"value":7}\n')
+    assert post(server, "/compute", "value=4294967301")[2] == '{"value":7}\n'  # int32(v), master.go:237
+    assert post(server, "/compute", "value=2147483647")[2] == '{"value":-2147483647}\n'
 
 
 @pytest.mark.gpu
