@@ -145,6 +145,37 @@ int mk_compute_device(mk_net *net, int device, const mk_input *in, size_t n, int
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats,
                       const mk_opts *opts, void *stream);
 
+/* ---- stateful sessions ------------------------
+ * The reference's nodes keep running between /compute calls
+ * (program.go:80-92): ACC, BAK, ptr, ports, stacks and the master's inChan /
+ * outChan (capacity 1, master.go:58-59) persist from one call to the next.
+ * A session set holds n such network instances in HBM, in the post-/reset,
+ * post-/run state; one compute call performs one /compute (master.go:
+ * 216-219) on every session at once: deposit in[i] once inChan is empty,
+ * run until outChan holds a value and take it.  status[i] is
+ * MK_ST_HAS_OUTPUT with out[i] the value, or the reason the call could not
+ * complete (MK_ST_QUIESCENT: the reference's handler would block forever;
+ * MK_ST_BUDGET: opts->budget retired instructions in this call;
+ * MK_ST_STACK_OVERFLOW); such a session stays ended (same status, no
+ * output) until mk_session_reset.  steps[i] (nullable): instructions retired
+ * in this call.  The mk_net must outlive its sessions. */
+typedef struct mk_session mk_session;
+
+int mk_session_create(mk_net *net, int device, size_t n, const mk_opts *opts, mk_session **out);
+
+/* One /compute call on every session (host arrays; synchronous). */
+int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps);
+
+/* The same on device arrays, asynchronous on `stream` (NULL = the session's
+ * own stream); calls on one session are ordered. */
+int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
+                              uint32_t *d_steps, void *stream);
+
+/* /reset (master.go:126-143): every session back to the initial state. */
+int mk_session_reset(mk_session *s);
+
+void mk_session_free(mk_session *s);
+
 /* Add the counters accumulated by MK_FLAG_DEFER_STATS launches on `device`
  * into d_stats (device uint64[MK_STATS_LEN]) and clear them; asynchronous
  * on `stream`.  Replaces nothing in the reference (it has no counters). */

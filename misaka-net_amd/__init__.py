@@ -10,6 +10,7 @@ from .network import (
     BatchResult,
     Network,
     NodeSpec,
+    SessionSet,
     TisParseError,
     generate_inputs_device,
     tokenize,
@@ -21,6 +22,7 @@ __all__ = [
     "BatchResult",
     "Network",
     "NodeSpec",
+    "SessionSet",
     "TisParseError",
     "generate_inputs_device",
     "tokenize",

@@ -103,6 +103,11 @@ SIGNATURES = {
         ],
     ),
     "mk_stats_fold": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "mk_session_create": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(mk_opts), C.POINTER(C.c_void_p)]),
+    "mk_session_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mk_session_compute_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mk_session_reset": (C.c_int, [C.c_void_p]),
+    "mk_session_free": (None, [C.c_void_p]),
     "mk_generate_inputs_device": (
         C.c_int,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p, C.c_void_p],

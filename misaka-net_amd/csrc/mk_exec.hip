@@ -768,6 +768,266 @@ __global__ void __launch_bounds__(B) tis_sched_tile(const DOp *__restrict__ code
     if (p.partials) write_partials(p.partials, gid, cnt);
 }
 
+// ------------------------------------------------------------------------
+// Stateful sessions.
+//
+// The reference's nodes keep running between /compute calls (program.go:
+// 80-92): ACC, BAK, ptr, ports, stacks and the master's inChan / outChan
+// (capacity 1 each, master.go:58-59) persist.  A session set is n network
+// instances whose state lives in HBM between calls (struct of arrays,
+// [field][session], coalesced); tis_session runs one /compute call on every
+// session, one thread each (oracle: tis_oracle.c session_call):
+//   loop: deposit the input once inChan is empty (m.inChan <- v, :216);
+//         take outChan's value once the input is deposited (:219) -> result;
+//         end the call at the per-call budget; run one round; a stack
+//         overflow or a round without change ends it.
+// A call without a result ends the session (the reference handler would
+// block forever): it reports that reason now and on every later call.
+// Ports are staged in LDS for the call; stack entries stay in HBM.
+// ------------------------------------------------------------------------
+struct SessParams {
+    uint32_t base[MK_MAX_PROGRAM_NODES];
+    uint32_t len[MK_MAX_PROGRAM_NODES];
+    int nprog;
+    int nstack;
+    uint64_t n;         // sessions
+    uint32_t budget;    // retired instructions per call
+    uint32_t stack_cap;
+    const int64_t *in;  // [n] this call's inputs (strconv.Atoi values)
+    int32_t *out;       // [n]
+    uint8_t *status;    // [n]
+    uint32_t *steps;    // [n] or null
+    int64_t *acc, *bak; // [nprog][n]
+    int32_t *ip, *pendv;  // [nprog][n]
+    int32_t *port;      // [nprog*4][n]
+    uint64_t *pfull;    // [n]
+    uint32_t *bits;     // [n]: pend (bits 0-15) | hung (bits 16-31)
+    uint32_t *io;       // [n]: in_full | out_full << 1 | dead << 4
+    int32_t *in_val, *out_val; // [n]
+    int32_t *sdepth;    // [nstack][n]
+    int32_t *stk;       // [nstack][stack_cap][n]
+};
+
+template <int NMAX>
+__global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ code, SessParams p)
+{
+    extern __shared__ int32_t lds[];
+    const int B = kBlock;
+    const int tid = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
+    const uint64_t n = p.n;
+    int32_t *const port = lds;                     // [nprog*4][B]
+    int32_t *const sdepth = lds + p.nprog * 4 * B; // [nstack][B]
+    const bool live = gid < n;
+
+    int64_t acc[NMAX], bak[NMAX];
+    int32_t ip[NMAX], pendv[NMAX];
+    uint64_t pfull = 0;
+    uint32_t pend = 0, hung = 0, io = 0;
+    int32_t in_val = 0, out_val = 0;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+        const bool on = live && k < p.nprog;
+        acc[k] = on ? p.acc[(uint64_t)k * n + gid] : 0;
+        bak[k] = on ? p.bak[(uint64_t)k * n + gid] : 0;
+        ip[k] = on ? p.ip[(uint64_t)k * n + gid] : 0;
+        pendv[k] = on ? p.pendv[(uint64_t)k * n + gid] : 0;
+    }
+    if (live) {
+        for (int q = 0; q < p.nprog * 4; ++q) port[q * B + tid] = p.port[(uint64_t)q * n + gid];
+        for (int q = 0; q < p.nstack; ++q) sdepth[q * B + tid] = p.sdepth[(uint64_t)q * n + gid];
+        pfull = p.pfull[gid];
+        const uint32_t bits = p.bits[gid];
+        pend = bits & 0xffffu;
+        hung = bits >> 16;
+        io = p.io[gid];
+        in_val = p.in_val[gid];
+        out_val = p.out_val[gid];
+    }
+    bool in_full = io & 1u, out_full = (io >> 1) & 1u;
+    uint32_t dead = (io >> 4) & 15u;
+    const int32_t x = live ? (int32_t)p.in[gid] : 0; // int32(v) at GetInput (master.go:237)
+    bool active = live && dead == 0, deposited = false, got = false;
+    int32_t result = 0;
+    uint32_t steps = 0;
+
+    for (;;) {
+        if (active) {
+            if (!deposited && !in_full) {
+                in_full = true;
+                in_val = x;
+                deposited = true;
+            }
+            if (deposited && out_full) {
+                out_full = false;
+                result = out_val;
+                got = true;
+                active = false;
+            } else if (steps >= p.budget) {
+                dead = MK_ST_BUDGET;
+                active = false;
+            }
+        }
+        if (!__ballot(active)) break;
+        bool changed = false, over = false;
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) {
+            if (k >= p.nprog) continue; // wave-uniform
+            const uint32_t len = p.len[k];
+            bool pending = active && !over && !((hung >> k) & 1u);
+            unsigned long long todo = __ballot(pending);
+            while (todo) {
+                const int lead = __builtin_ctzll(todo);
+                const int u = __builtin_amdgcn_readlane(ip[k], lead);
+                const bool mine = pending && ip[k] == u;
+                todo &= ~__ballot(mine);
+                const Insn I = fetch(code, p.base[k] + (uint32_t)u);
+                if (!mine) continue;
+                pending = false;
+                auto retire = [&]() {
+                    ip[k] = (ip[k] + 1 == (int32_t)len) ? 0 : ip[k] + 1; // program.go:429
+                    ++steps;
+                    changed = true;
+                };
+                auto jump = [&](int32_t t) {
+                    ip[k] = t;
+                    ++steps;
+                    changed = true;
+                };
+                switch (I.op) {
+                case OP_NOP: retire(); break;
+                case OP_SWP: { const int64_t t = acc[k]; acc[k] = bak[k]; bak[k] = t; retire(); break; }
+                case OP_SAV: bak[k] = acc[k]; retire(); break;
+                case OP_NEG: acc[k] = (int64_t)(0ull - (uint64_t)acc[k]); retire(); break;
+                case OP_JMP: jump(I.arg); break;
+                case OP_JEZ: if (acc[k] == 0) jump(I.arg); else retire(); break;
+                case OP_JNZ: if (acc[k] != 0) jump(I.arg); else retire(); break;
+                case OP_JGZ: if (acc[k] > 0) jump(I.arg); else retire(); break;
+                case OP_JLZ: if (acc[k] < 0) jump(I.arg); else retire(); break;
+                case OP_STUCK: break;
+                case OP_IN:
+                    if (in_full) { // <-m.inChan (master.go:235)
+                        in_full = false;
+                        if (I.dst) acc[k] = in_val;
+                        retire();
+                    }
+                    break;
+                case OP_POP: {
+                    int32_t *dp = &sdepth[I.arg * B + tid];
+                    const int32_t d = *dp;
+                    if (d > 0) { // waitPop blocks while empty (stack.go:133-155)
+                        const int32_t v = p.stk[((uint64_t)I.arg * p.stack_cap + (uint32_t)(d - 1)) * n + gid];
+                        *dp = d - 1;
+                        if (I.dst) acc[k] = v;
+                        retire();
+                    }
+                    break;
+                }
+                default: {
+                    // Ops with a source operand: getFromSrc (program.go:434-472).
+                    const bool pn = (pend >> k) & 1u;
+                    int64_t v = 0;
+                    bool consumed = false;
+                    if (pn) {
+                        v = pendv[k];
+                    } else if (I.src == SRC_IMM) {
+                        v = I.imm;
+                    } else if (I.src == SRC_ACC) {
+                        v = acc[k];
+                    } else if (I.src >= SRC_R0) {
+                        const uint32_t slot = (uint32_t)k * 4 + (I.src - SRC_R0);
+                        if (!((pfull >> slot) & 1ull)) break; // receive blocks
+                        v = port[slot * B + tid];
+                        pfull &= ~(1ull << slot);
+                        consumed = true;
+                    }
+                    switch (I.op) {
+                    case OP_MOV: if (I.dst) acc[k] = v; retire(); break;
+                    case OP_ADD: acc[k] = (int64_t)((uint64_t)acc[k] + (uint64_t)v); retire(); break;
+                    case OP_SUB: acc[k] = (int64_t)((uint64_t)acc[k] - (uint64_t)v); retire(); break;
+                    case OP_JRO: {
+                        int64_t t = (int64_t)((uint64_t)(int64_t)ip[k] + (uint64_t)v);
+                        t = t > (int64_t)len - 1 ? (int64_t)len - 1 : t;
+                        t = t < 0 ? 0 : t;
+                        jump((int32_t)t);
+                        break;
+                    }
+                    case OP_SEND: {
+                        const uint32_t slot = I.arg;
+                        if (!((pfull >> slot) & 1ull)) {
+                            port[slot * B + tid] = (int32_t)v;
+                            pfull |= 1ull << slot;
+                            pend &= ~(1u << k);
+                            retire();
+                        } else if (!pn) {
+                            pend |= 1u << k;
+                            pendv[k] = (int32_t)v;
+                            changed = true;
+                        }
+                        break;
+                    }
+                    case OP_OUT: // outChan <- v blocks while full (master.go:246)
+                        if (!out_full) {
+                            out_full = true;
+                            out_val = (int32_t)v;
+                            pend &= ~(1u << k);
+                            retire();
+                        } else if (!pn) {
+                            pend |= 1u << k;
+                            pendv[k] = (int32_t)v;
+                            changed = true;
+                        }
+                        break;
+                    case OP_PUSH: {
+                        int32_t *dp = &sdepth[I.arg * B + tid];
+                        const uint32_t d = (uint32_t)*dp;
+                        if (d >= p.stack_cap) { over = true; break; }
+                        p.stk[((uint64_t)I.arg * p.stack_cap + d) * n + gid] = (int32_t)v; // int32(v), program.go:516
+                        *dp = (int32_t)(d + 1);
+                        retire();
+                        break;
+                    }
+                    case OP_HANG: hung |= 1u << k; changed = true; break;
+                    case OP_RETRY: if (consumed) changed = true; break;
+                    default: break;
+                    }
+                    break;
+                }
+                }
+            }
+        }
+        if (active) {
+            if (over) {
+                dead = MK_ST_STACK_OVERFLOW;
+                active = false;
+            } else if (!changed) {
+                dead = MK_ST_QUIESCENT;
+                active = false;
+            }
+        }
+    }
+
+    if (!live) return;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+        if (k >= p.nprog) continue;
+        p.acc[(uint64_t)k * n + gid] = acc[k];
+        p.bak[(uint64_t)k * n + gid] = bak[k];
+        p.ip[(uint64_t)k * n + gid] = ip[k];
+        p.pendv[(uint64_t)k * n + gid] = pendv[k];
+    }
+    for (int q = 0; q < p.nprog * 4; ++q) p.port[(uint64_t)q * n + gid] = port[q * B + tid];
+    for (int q = 0; q < p.nstack; ++q) p.sdepth[(uint64_t)q * n + gid] = sdepth[q * B + tid];
+    p.pfull[gid] = pfull;
+    p.bits[gid] = (pend & 0xffffu) | (hung << 16);
+    p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (dead << 4);
+    p.in_val[gid] = in_val;
+    p.out_val[gid] = out_val;
+    p.out[gid] = got ? result : 0;
+    p.status[gid] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : dead);
+    if (p.steps) p.steps[gid] = steps;
+}
+
 __global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
                                                      uint64_t offset, uint64_t n, int32_t *out)
 {
@@ -1376,6 +1636,67 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
 
+// ---- stateful sessions: host side -----------------------------------------
+template <int NMAX>
+void *session_kernel_ptr() { return reinterpret_cast<void *>(&tis_session<NMAX>); }
+
+void *pick_session_kernel(int nprog)
+{
+    if (nprog <= 1) return session_kernel_ptr<1>();
+    if (nprog <= 2) return session_kernel_ptr<2>();
+    if (nprog <= 4) return session_kernel_ptr<4>();
+    if (nprog <= 8) return session_kernel_ptr<8>();
+    return session_kernel_ptr<16>();
+}
+
+} // namespace
+} // namespace mk
+
+struct mk_session {
+    mk_net *h = nullptr;
+    int device = 0;
+    size_t n = 0;
+    uint32_t budget = 0, cap = 0;
+    int nprog = 0, nstack = 0;
+    std::mutex mu;
+    void *d_state = nullptr; // every per-session array, one allocation
+    size_t state_bytes = 0;
+    void *d_stage = nullptr; // host-API staging: in, out, status, steps
+    hipStream_t stream = nullptr;
+    mk::SessParams p{};
+    ~mk_session()
+    {
+        mk::DeviceGuard g(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipFree(d_state);
+        (void)hipFree(d_stage);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace mk {
+namespace {
+
+int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
+                   hipStream_t stream)
+{
+    if (s->n == 0) return MK_OK;
+    SessParams p = s->p;
+    p.in = d_in;
+    p.out = d_out;
+    p.status = d_status;
+    p.steps = d_steps;
+    const Insn *code = s->h->dev[s->device].d_code;
+    const size_t lds = (size_t)(s->nprog * 4 + s->nstack) * kBlock * 4;
+    const uint64_t blocks = (s->n + kBlock - 1) / kBlock;
+    if (blocks > 0x7fffffffull) return MK_ELIMIT;
+    void *args[] = {(void *)&code, (void *)&p};
+    if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)blocks), dim3(kBlock), args, lds, stream) !=
+        hipSuccess)
+        return MK_EDEVICE;
+    return MK_OK;
+}
+
 void set_err(char *err, size_t len, const std::string &s)
 {
     if (!err || !len) return;
@@ -1508,6 +1829,128 @@ int mk_compute_device(mk_net *h, int device, const mk_input *in, size_t n, int32
     std::lock_guard<std::mutex> lk(h->mu);
     return mk::launch_locked(h, device, in, n, d_out, d_status, d_steps, d_stats, opts, (hipStream_t)stream);
 }
+
+int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_session **out)
+{
+    if (!h || !out) return MK_EINVAL;
+    *out = nullptr;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev || device >= mk::kMaxDevices) return MK_EINVAL;
+    uint32_t budget, cap, flags;
+    mk::resolve_opts(opts, budget, cap, flags);
+    std::unique_ptr<mk_session> s(new (std::nothrow) mk_session());
+    if (!s) return MK_ENOMEM;
+    s->h = h;
+    s->device = device;
+    s->n = n;
+    s->budget = budget;
+    s->cap = cap;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        int rc = mk::ensure_device(h, device);
+        if (rc) return rc;
+        s->nprog = h->net.nprog;
+        s->nstack = h->net.uses_stacks ? h->net.nstack : 0;
+    }
+    mk::DeviceGuard g(device);
+    // one allocation, 256-byte aligned arrays, [field][session]
+    const size_t N = n ? n : 1, P = (size_t)s->nprog, S = (size_t)s->nstack;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t sz[] = {al(P * N * 8), al(P * N * 8), al(P * N * 4), al(P * N * 4), al(P * 4 * N * 4), al(N * 8),
+                         al(N * 4),     al(N * 4),     al(N * 4),     al(N * 4),     al(S * N * 4),     al(S * cap * N * 4)};
+    size_t total = 0;
+    for (size_t b : sz) total += b;
+    if (hipMalloc(&s->d_state, total) != hipSuccess) return MK_ENOMEM;
+    s->state_bytes = total;
+    char *b = (char *)s->d_state;
+    size_t off = 0;
+    auto take = [&](size_t i) { char *q = b + off; off += sz[i]; return q; };
+    mk::SessParams &p = s->p;
+    for (int i = 0; i < s->nprog; i++) {
+        p.base[i] = h->net.base[i];
+        p.len[i] = h->net.len[i];
+    }
+    p.nprog = s->nprog;
+    p.nstack = s->nstack;
+    p.n = n;
+    p.budget = budget;
+    p.stack_cap = cap;
+    p.acc = (int64_t *)take(0);
+    p.bak = (int64_t *)take(1);
+    p.ip = (int32_t *)take(2);
+    p.pendv = (int32_t *)take(3);
+    p.port = (int32_t *)take(4);
+    p.pfull = (uint64_t *)take(5);
+    p.bits = (uint32_t *)take(6);
+    p.io = (uint32_t *)take(7);
+    p.in_val = (int32_t *)take(8);
+    p.out_val = (int32_t *)take(9);
+    p.sdepth = (int32_t *)take(10);
+    p.stk = (int32_t *)take(11);
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return MK_EDEVICE;
+    if (hipMemsetAsync(s->d_state, 0, total, s->stream) != hipSuccess) return MK_EDEVICE; // post-/reset state
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
+    *out = s.release();
+    return MK_OK;
+}
+
+int mk_session_reset(mk_session *s)
+{
+    if (!s) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    if (hipMemsetAsync(s->d_state, 0, s->state_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
+    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+
+int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
+                              uint32_t *d_steps, void *stream)
+{
+    if (!s || (s->n && (!d_in || !d_out || !d_status))) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    // the session state is ordered on the session's own stream
+    if (stream && hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
+    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st);
+    if (rc) return rc;
+    if (stream) {
+        hipEvent_t ev;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
+        (void)hipEventRecord(ev, st);
+        (void)hipStreamWaitEvent(s->stream, ev, 0);
+        (void)hipEventDestroy(ev);
+    }
+    return MK_OK;
+}
+
+int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps)
+{
+    if (!s || (s->n && (!in || !out || !status))) return MK_EINVAL;
+    if (s->n == 0) return MK_OK;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    const size_t n = s->n;
+    const size_t a8 = (n * 8 + 255) & ~(size_t)255, a4 = (n * 4 + 255) & ~(size_t)255;
+    if (!s->d_stage && hipMalloc(&s->d_stage, a8 + a4 + a4 + n) != hipSuccess) return MK_ENOMEM;
+    char *b = (char *)s->d_stage;
+    int64_t *din = (int64_t *)b;
+    int32_t *dout = (int32_t *)(b + a8);
+    uint32_t *dsteps = (uint32_t *)(b + a8 + a4);
+    uint8_t *dst = (uint8_t *)(b + a8 + a4 + a4);
+    if (hipMemcpyAsync(din, in, n * 8, hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
+    int rc = mk::session_launch(s, din, dout, dst, steps ? dsteps : nullptr, s->stream);
+    if (rc) return rc;
+    if (hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+        hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+        return MK_EDEVICE;
+    if (steps && hipMemcpyAsync(steps, dsteps, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+        return MK_EDEVICE;
+    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+
+void mk_session_free(mk_session *s) { delete s; }
 
 int mk_stats_fold(mk_net *h, int device, uint64_t *d_stats, void *stream)
 {

@@ -250,10 +250,61 @@ class Network:
         launch.keep = (mi, o, self)
         return launch
 
+    def sessions(self, n, *, device=0, budget=None, stack_cap=None) -> "SessionSet":
+        """``n`` stateful instances of this network (row f2, :class:`SessionSet`)."""
+        return SessionSet(self, n, device=device, budget=budget, stack_cap=stack_cap)
+
     def stats_fold(self, stats_ptr, *, device=0, stream=None):
         """Add the counters of deferred launches on ``device`` into the
         device uint64[MK_STATS_LEN] at ``stats_ptr`` (asynchronous)."""
         N.check(N.lib().mk_stats_fold(self._h, device, stats_ptr, stream), "mk_stats_fold")
+
+
+class SessionSet:
+    """``n`` stateful instances of a network on one GPU (SURVEY.md section 8
+    row f2).  The reference's nodes keep running between /compute calls
+    (program.go:80-92); here each instance's ACC/BAK/ptr, ports, stacks and the
+    master's inChan/outChan persist in HBM between calls, and :meth:`compute`
+    performs one /compute (master.go:216-219) on every instance at once."""
+
+    def __init__(self, net: "Network", n: int, *, device: int = 0, budget=None, stack_cap=None):
+        o = make_opts(budget, stack_cap)
+        h = C.c_void_p()
+        N.check(N.lib().mk_session_create(net.handle, device, n, C.byref(o), C.byref(h)), "mk_session_create")
+        self._h, self._net, self.n, self.device = h, net, n, device
+
+    def compute(self, values, *, steps=True) -> BatchResult:
+        """One /compute call per instance: ``values[i]`` goes to instance i."""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        if v.size != self.n:
+            raise ValueError(f"expected {self.n} values, got {v.size}")
+        out = np.zeros(self.n, np.int32)
+        st = np.zeros(self.n, np.uint8)
+        sp = np.zeros(self.n, np.uint32) if steps else None
+        N.check(N.lib().mk_session_compute(self._h, v.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+                                           st.ctypes.data_as(C.c_void_p),
+                                           sp.ctypes.data_as(C.c_void_p) if sp is not None else None),
+                "mk_session_compute")
+        return BatchResult(out, st, sp)
+
+    def compute_device(self, in_ptr, out_ptr, status_ptr, steps_ptr=None, *, stream=None):
+        N.check(N.lib().mk_session_compute_device(self._h, in_ptr, out_ptr, status_ptr, steps_ptr, stream),
+                "mk_session_compute_device")
+
+    def reset(self):
+        """/reset (master.go:126-143): every instance back to its initial state."""
+        N.check(N.lib().mk_session_reset(self._h), "mk_session_reset")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().mk_session_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def generate_inputs_device(n, out_ptr, *, seed, gen_kind=N.MK_GEN_FULL, gen_mask=0, offset=0, device=0, stream=None):

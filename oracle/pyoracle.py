@@ -65,6 +65,12 @@ def lib():
             C.c_int,
         ]
         h.orc_gen_inputs.argtypes = [C.c_uint64, C.c_int, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p]
+        h.orc_sessions_new.restype = C.c_void_p
+        h.orc_sessions_new.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+        h.orc_sessions_free.argtypes = [C.c_void_p]
+        h.orc_sessions_reset.argtypes = [C.c_void_p]
+        h.orc_sessions_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                           C.c_int]
         h.orc_go_atoi.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64)]
         _lib = h
     return _lib
@@ -147,6 +153,36 @@ class OracleNet:
             1 if stop_on_output else 0,
             threads,
         )
+        assert rc == 0
+        return out, st, sp
+
+
+class OracleSessions:
+    """n stateful network instances (row f2): each compute() is one /compute
+    call on every instance; state persists between calls (see tis_oracle.c)."""
+
+    def __init__(self, net: OracleNet, n: int, *, stack_cap: Optional[int] = None):
+        self._net = net  # keeps the network alive
+        self.n = n
+        self._h = lib().orc_sessions_new(net._h, n, 1024 if stack_cap is None else stack_cap)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_sessions_free(self._h)
+            self._h = None
+
+    def reset(self):
+        lib().orc_sessions_reset(self._h)
+
+    def compute(self, values, *, budget: Optional[int] = None, threads: int = 1):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        assert v.size == self.n
+        out = np.zeros(self.n, np.int32)
+        st = np.zeros(self.n, np.uint8)
+        sp = np.zeros(self.n, np.uint32)
+        rc = lib().orc_sessions_compute(self._h, v.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+                                        st.ctypes.data_as(C.c_void_p), sp.ctypes.data_as(C.c_void_p),
+                                        budget or (1 << 20), threads)
         assert rc == 0
         return out, st, sp
 

@@ -628,6 +628,11 @@ typedef struct {
     int64_t out_val;
     uint32_t steps;
     uint32_t stack_cap;
+    /* stateful sessions (row f2): outChan is a capacity-1 channel emptied by
+     * each /compute, instead of the single-/compute out_cnt rule */
+    int session;
+    int out_full;
+    uint8_t dead; /* reason the session ended (0 = alive) */
 } lane_t;
 
 enum { R_NONE = 0, R_CHANGED = 1, R_RETIRED = 3, R_OVERFLOW = 4 };
@@ -692,6 +697,19 @@ static int net_send(const orc_net *net, lane_t *ln, pnode_t *nd, int64_t v, cons
 /* outputValue (program.go:554-566) + Master.SendOutput (master.go:245-249). */
 static int net_out(lane_t *ln, pnode_t *nd, int64_t v)
 {
+    if (ln->session) { /* outChan <- v blocks while full (master.go:246, cap 1 :59) */
+        if (ln->out_full) {
+            if (nd->pend)
+                return R_NONE;
+            nd->pend = 1;
+            nd->pendval = v;
+            return R_CHANGED;
+        }
+        ln->out_full = 1;
+        ln->out_val = (int64_t)(int32_t)v;
+        nd->pend = 0;
+        return R_RETIRED;
+    }
     if (ln->out_cnt >= 2) { /* outChan (cap 1) full and /compute reads only once */
         if (nd->pend)
             return R_NONE;
@@ -973,6 +991,166 @@ int orc_compute_batch(const orc_net *net, const int64_t *in, size_t n, int32_t *
     }
     for (int t = 0; t < threads; t++)
         pthread_create(&tid[t], NULL, worker, &jobs[t]);
+    for (int t = 0; t < threads; t++)
+        pthread_join(tid[t], NULL);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Stateful sessions                            */
+/* ------------------------------------------------------------------------ */
+/* The reference's nodes keep running between /compute calls
+ * (program.go:80-92): ACC, BAK, ptr, ports, stacks and the master's inChan /
+ * outChan (capacity 1 each, master.go:58-59) persist from one call to the
+ * next.  A session is one network instance under the canonical schedule; one
+ * /compute call (master.go:216-219) on it:
+ *   loop:
+ *     if inChan is empty and the input is not deposited yet: deposit it
+ *       (m.inChan <- v blocks while inChan is full, :216);
+ *     if it is deposited and outChan holds a value: take it -> the result
+ *       (<-m.outChan, :219);
+ *     if the call's retired instructions reached the budget: the call ends;
+ *     run one round; a stack overflow or a round without change ends it.
+ * A call that ends without a result (the reference handler would block
+ * forever) ends the session: that call and every later one report the
+ * reason without output, until the session is reset. */
+typedef struct {
+    const orc_net *net;
+    size_t n;
+    lane_t **lanes;
+} orc_sessions;
+
+static void lane_reset_session(const orc_net *net, lane_t *ln)
+{
+    lane_reset(net, ln, 0);
+    ln->in_avail = 0; /* inChan empty */
+    ln->session = 1;
+    ln->out_full = 0;
+    ln->dead = 0;
+}
+
+static uint8_t session_call(const orc_net *net, lane_t *ln, int64_t x, uint32_t budget, int32_t *out,
+                            uint32_t *steps)
+{
+    *out = 0;
+    *steps = 0;
+    if (ln->dead)
+        return ln->dead;
+    const uint32_t s0 = ln->steps;
+    int deposited = 0;
+    for (;;) {
+        if (!deposited && !ln->in_avail) {
+            ln->in_avail = 1;
+            ln->in_val = x;
+            deposited = 1;
+        }
+        if (deposited && ln->out_full) {
+            ln->out_full = 0;
+            *out = (int32_t)ln->out_val;
+            *steps = ln->steps - s0;
+            return ST_HAS_OUTPUT;
+        }
+        if (ln->steps - s0 >= budget) {
+            ln->dead = ST_BUDGET;
+            break;
+        }
+        int changed = 0, over = 0;
+        for (int n = 0; n < net->nprog; n++) {
+            int r = attempt(net, ln, n);
+            if (r & R_OVERFLOW) {
+                over = 1;
+                break;
+            }
+            changed |= r & R_CHANGED;
+        }
+        if (over) {
+            ln->dead = ST_STACK_OVERFLOW;
+            break;
+        }
+        if (!changed) {
+            ln->dead = ST_QUIESCENT;
+            break;
+        }
+    }
+    *steps = ln->steps - s0;
+    return ln->dead;
+}
+
+orc_sessions *orc_sessions_new(const orc_net *net, size_t n, uint32_t stack_cap)
+{
+    orc_sessions *S = (orc_sessions *)calloc(1, sizeof(orc_sessions));
+    S->net = net;
+    S->n = n;
+    S->lanes = (lane_t **)calloc(n ? n : 1, sizeof(lane_t *));
+    for (size_t i = 0; i < n; i++) {
+        S->lanes[i] = lane_alloc(net, stack_cap);
+        lane_reset_session(net, S->lanes[i]);
+    }
+    return S;
+}
+
+void orc_sessions_free(orc_sessions *S)
+{
+    if (!S)
+        return;
+    for (size_t i = 0; i < S->n; i++)
+        lane_free(S->net, S->lanes[i]);
+    free(S->lanes);
+    free(S);
+}
+
+void orc_sessions_reset(orc_sessions *S)
+{
+    for (size_t i = 0; i < S->n; i++)
+        lane_reset_session(S->net, S->lanes[i]);
+}
+
+typedef struct {
+    orc_sessions *S;
+    const int64_t *in;
+    int32_t *out;
+    uint8_t *status;
+    uint32_t *steps;
+    uint32_t budget;
+    size_t lo, hi;
+} sjob_t;
+
+static void *sworker(void *arg)
+{
+    sjob_t *j = (sjob_t *)arg;
+    for (size_t i = j->lo; i < j->hi; i++) {
+        uint32_t sp;
+        j->status[i] = session_call(j->S->net, j->S->lanes[i], j->in[i], j->budget, &j->out[i], &sp);
+        if (j->steps)
+            j->steps[i] = sp;
+    }
+    return NULL;
+}
+
+/* One /compute call on every session i with input in[i]. */
+int orc_sessions_compute(orc_sessions *S, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps,
+                         uint32_t budget, int threads)
+{
+    if (!S || budget == 0)
+        return -1;
+    const size_t n = S->n;
+    if (threads < 1)
+        threads = 1;
+    if ((size_t)threads > n)
+        threads = n ? (int)n : 1;
+    if (threads > 256)
+        threads = 256;
+    sjob_t jobs[256];
+    pthread_t tid[256];
+    for (int t = 0; t < threads; t++)
+        jobs[t] = (sjob_t){S, in, out, status, steps, budget, n * (size_t)t / (size_t)threads,
+                           n * (size_t)(t + 1) / (size_t)threads};
+    if (threads == 1) {
+        sworker(&jobs[0]);
+        return 0;
+    }
+    for (int t = 0; t < threads; t++)
+        pthread_create(&tid[t], NULL, sworker, &jobs[t]);
     for (int t = 0; t < threads; t++)
         pthread_join(tid[t], NULL);
     return 0;

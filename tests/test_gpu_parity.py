@@ -307,3 +307,50 @@ def test_deferred_stats_fold(gpu, mode):
     assert s_imm.tolist() == s_def.tolist()
     steps = sum(int(oracle(nodes, po.gen_inputs(seed, n, kind=1, mask=1023))[2].sum()) for seed in (1, 2, 3))
     assert s_def[0].item() == steps and s_def[2].item() == 3 * n
+
+
+# ---- stateful sessions (row f2): GPU vs the oracle's session restatement ----
+def _session_pair(nodes, n, **kw):
+    cap = kw.get("stack_cap")
+    g = mk.Network(nodes).sessions(n, budget=kw.get("budget"), stack_cap=cap)
+    o = po.OracleSessions(po.OracleNet(nodes), n, stack_cap=cap)
+    return g, o
+
+
+def _session_calls(nodes, seqs, **kw):
+    g, o = _session_pair(nodes, seqs.shape[1], **kw)
+    for k, row in enumerate(seqs):
+        got = g.compute(row)
+        assert_same(got, o.compute(row, budget=kw.get("budget"), threads=THREADS), f"call {k}")
+    return g, o
+
+
+def test_sessions_example_network(gpu):
+    seqs = po.gen_inputs(SEED, 6 * 3000).reshape(6, 3000)
+    g, _ = _session_calls(mk.networks.example_network(), seqs)
+    r = g.compute(np.full(3000, 5))
+    assert (r.out == 7).all() and (r.status == N.MK_ST_HAS_OUTPUT).all()
+
+
+def test_sessions_countdown_and_reset(gpu):
+    nodes = mk.networks.countdown_network()
+    seqs = po.gen_inputs(SEED, 4 * 2000, kind=1, mask=1023).reshape(4, 2000)
+    g, o = _session_calls(nodes, seqs, budget=3000)
+    g.reset()
+    o.reset()
+    row = po.gen_inputs(7, 2000, kind=1, mask=1023)
+    assert_same(g.compute(row), o.compute(row, budget=3000), "after reset")
+
+
+@pytest.mark.parametrize("seed", range(0, 60))
+def test_sessions_random_networks(gpu, seed):
+    rows = random_network(seed)
+    cap = [1, 3, 8, 16, 17, 40, 1024][seed % 7]
+    seqs = po.gen_inputs(seed * 131 + 5, 5 * 300).reshape(5, 300)
+    _session_calls(rows, seqs, budget=[37, 200, 1000][seed % 3], stack_cap=cap)
+
+
+def test_sessions_deep_stacks(gpu):
+    nodes = mk.networks.pipeline_network(64)
+    seqs = po.gen_inputs(SEED, 3 * 500).reshape(3, 500)
+    _session_calls(nodes, seqs)
