@@ -17,8 +17,11 @@ Deliberate differences (DESIGN.md / INTEGRATION.md):
     program nodes serve :8001, master.go:178, so its /load never completes);
     a rejected program answers 400 "error loading program on node X: <Go
     error text>" and leaves the previous program in place (program.go:180-192).
-  * every /compute runs on a fresh post-/reset copy of the network (the lane
-    model); the reference keeps node state between calls (row f2, next).
+  * by default every /compute runs on a fresh post-/reset copy of the network
+    (the lane model: independent inputs, batchable).  ``stateful=True`` keeps
+    the reference's semantics instead (row f2): one network instance whose
+    node state, stacks and channels persist across /compute calls, on the GPU
+    (SessionSet); /reset and /load reset it, /pause keeps it.
   * a /compute whose network produces no output answers 504 "network
     produced no output" instead of hanging forever.
 """
@@ -96,7 +99,7 @@ class MasterNode:
     """
 
     def __init__(self, node_info: Mapping[str, Mapping], programs: Optional[Mapping[str, str]] = None,
-                 name: str = "last_order", devices=None, budget=None, stack_cap=None):
+                 name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = False):
         self.node_info = {k: dict(v) for k, v in node_info.items()}
         self.name = name
         self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
@@ -113,6 +116,8 @@ class MasterNode:
                 except TisParseError:
                     pass
         self._net = None
+        self.stateful = stateful
+        self._sess = None
 
     # -- network handle ------------------------------------------------------
     def _specs(self):
@@ -129,6 +134,27 @@ class MasterNode:
         if self._net is None:
             self._net = Network(self._specs())
         return self._net
+
+    def session(self):
+        """The one persistent network instance of stateful mode."""
+        if self._sess is None:
+            dev = next(iter(self.devices), 0) if self.devices else 0
+            self._sess = self.network().sessions(1, device=dev, budget=self.budget, stack_cap=self.stack_cap)
+        return self._sess
+
+    def _drop_state(self):
+        if self._sess is not None:
+            self._sess.close()
+            self._sess = None
+
+    def _call(self, v: int):
+        """One /compute: (has_output, value)."""
+        if self.stateful:
+            r = self.session().compute([v], steps=False)
+        else:
+            r = self.network().compute_batch([v], budget=self.budget, stack_cap=self.stack_cap,
+                                             devices=self.devices, steps=False)
+        return bool(int(r.status[0]) & N.MK_ST_HAS_OUTPUT), int(r.out[0])
 
     # -- handlers -------------------------------------------------------------
     def handle(self, method: str, path: str, query: str = "", body: bytes = b"", ctype: str = "") -> Response:
@@ -177,6 +203,7 @@ class MasterNode:
             if e:
                 return http_error(f"error resetting network: {e}", 400)
             self.is_running = False
+            self._drop_state()  # resetNode on every node and the master's channels (master.go:129-138)
             return Response(200, "Success")
 
     def _load(self, query, body, ctype):
@@ -201,6 +228,7 @@ class MasterNode:
             except TisParseError as ex:
                 return http_error(f"error loading program on node {target}: {ex}", 400)
             self.programs[target] = program
+            self._drop_state()
             if self._net is not None:
                 self._net.close()
                 self._net = None
@@ -221,12 +249,11 @@ class MasterNode:
         except ValueError:
             return http_error("cannot parse value", 400)
         with self._lock:
-            r = self.network().compute_batch([v], budget=self.budget, stack_cap=self.stack_cap,
-                                             devices=self.devices, steps=False)
-        if not (int(r.status[0]) & N.MK_ST_HAS_OUTPUT):
+            ok, out = self._call(v)
+        if not ok:
             return http_error("network produced no output", 504)
         # json.NewEncoder(w).Encode(clientOutResponse{...}) (master.go:219): compact, newline-terminated
-        return Response(200, json.dumps({"value": int(r.out[0])}, separators=(",", ":")) + "\n", "application/json")
+        return Response(200, json.dumps({"value": out}, separators=(",", ":")) + "\n", "application/json")
 
     def _compute_batch(self, query, body, ctype):
         if not self.is_running:
@@ -244,10 +271,16 @@ class MasterNode:
         except (ValueError, TypeError, AttributeError):
             return http_error("cannot parse value", 400)
         with self._lock:
-            r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
-                                             stack_cap=self.stack_cap, devices=self.devices, steps=False)
-        has = (r.status & N.MK_ST_HAS_OUTPUT) != 0
-        out = {"values": [int(x) if h else None for x, h in zip(r.out, has)], "status": r.status.tolist()}
+            if self.stateful:  # sequential /compute calls on the one instance
+                res = [self.session().compute([v], steps=False) for v in vals]
+                outs = [int(r.out[0]) for r in res]
+                sts = [int(r.status[0]) for r in res]
+            else:
+                r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
+                                                 stack_cap=self.stack_cap, devices=self.devices, steps=False)
+                outs, sts = r.out.tolist(), r.status.tolist()
+        has = [(x & N.MK_ST_HAS_OUTPUT) != 0 for x in sts]
+        out = {"values": [x if h else None for x, h in zip(outs, has)], "status": sts}
         return Response(200, json.dumps(out) + "\n", "application/json")
 
 

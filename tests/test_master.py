@@ -127,3 +127,27 @@ def test_http_compute_batch_and_load(server):
     assert post(server, "/load", "program=IN+ACC&targetURI=misaka1")[0] == 200
     post(server, "/run")
     assert post(server, "/compute", "value=1")[:1] == (504,)
+
+
+@pytest.mark.gpu
+def test_stateful_master_keeps_node_state(gpu):
+    # row f2: a running sum survives between /compute calls, /pause keeps it,
+    # /reset clears it (program.go:80-92, 207-216; master.go:126-143)
+    m = MasterNode({"acc": {"type": "program"}}, {"acc": "IN NIL\nADD 10\nOUT ACC"}, stateful=True)
+    m.handle("POST", "/run")
+    vals = [m.handle("POST", "/compute", body=b"value=0", ctype=FORM).body for _ in range(3)]
+    assert vals == ['{"value":10}\n', '{"value":20}\n', '{"value":30}\n']
+    m.handle("POST", "/pause")
+    assert m.handle("POST", "/compute", body=b"value=0", ctype=FORM).code == 400
+    m.handle("POST", "/run")
+    assert m.handle("POST", "/compute", body=b"value=0", ctype=FORM).body == '{"value":40}\n'
+    m.handle("POST", "/reset")
+    m.handle("POST", "/run")
+    assert m.handle("POST", "/compute", body=b"value=0", ctype=FORM).body == '{"value":10}\n'
+    r = m.handle("POST", "/compute_batch", body=b"value=0&value=0", ctype=FORM)
+    assert json.loads(r.body)["values"] == [20, 30]
+    # the example network is stateless in effect: x + 2 on every call
+    e = MasterNode(NODE_INFO, PROGRAMS, stateful=True)
+    e.handle("POST", "/run")
+    assert [e.handle("POST", "/compute", body=f"value={x}".encode(), ctype=FORM).body for x in (5, 6)] == \
+        ['{"value":7}\n', '{"value":8}\n']
