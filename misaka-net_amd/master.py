@@ -22,6 +22,12 @@ Deliberate differences (DESIGN.md / INTEGRATION.md):
     the reference's semantics instead (row f2): one network instance whose
     node state, stacks and channels persist across /compute calls, on the GPU
     (SessionSet); /reset and /load reset it, /pause keeps it.
+  * ``wire=MasterService`` (misaka_net_amd.wire, row f4): /compute goes over
+    the reference's gRPC wire instead -- inChan/outChan served as
+    grpc.Master.GetInput/SendOutput to external (reference) program nodes,
+    exactly master.go:216-219; /pause cancels blocked calls, /reset renews
+    the channels.  ``wire_timeout`` bounds the wait (504), the reference has
+    none.
   * a /compute whose network produces no output answers 504 "network
     produced no output" instead of hanging forever.
 """
@@ -99,7 +105,8 @@ class MasterNode:
     """
 
     def __init__(self, node_info: Mapping[str, Mapping], programs: Optional[Mapping[str, str]] = None,
-                 name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = False):
+                 name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = False,
+                 wire=None, wire_timeout: Optional[float] = 30.0):
         self.node_info = {k: dict(v) for k, v in node_info.items()}
         self.name = name
         self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
@@ -118,6 +125,7 @@ class MasterNode:
         self._net = None
         self.stateful = stateful
         self._sess = None
+        self.wire, self.wire_timeout = wire, wire_timeout
 
     # -- network handle ------------------------------------------------------
     def _specs(self):
@@ -149,6 +157,11 @@ class MasterNode:
 
     def _call(self, v: int):
         """One /compute: (has_output, value)."""
+        if self.wire is not None:
+            try:
+                return True, self.wire.compute(v, timeout=self.wire_timeout)
+            except Exception:  # timeout or cancelled by /pause, /reset
+                return False, 0
         if self.stateful:
             r = self.session().compute([v], steps=False)
         else:
@@ -195,6 +208,8 @@ class MasterNode:
             if e:
                 return http_error(f"error pausing network: {e}", 400)
             self.is_running = False
+            if self.wire is not None:
+                self.wire.cancel()  # stopNode: blocked GetInput calls return errors (master.go:117-119, 251-260)
             return Response(200, "Success")
 
     def _reset(self, *_):
@@ -204,6 +219,8 @@ class MasterNode:
                 return http_error(f"error resetting network: {e}", 400)
             self.is_running = False
             self._drop_state()  # resetNode on every node and the master's channels (master.go:129-138)
+            if self.wire is not None:
+                self.wire.reset()
             return Response(200, "Success")
 
     def _load(self, query, body, ctype):
@@ -248,8 +265,11 @@ class MasterNode:
             v = go_atoi(self._values(form)[0])
         except ValueError:
             return http_error("cannot parse value", 400)
-        with self._lock:
+        if self.wire is not None:  # concurrent handlers, like net/http (master.go:197)
             ok, out = self._call(v)
+        else:
+            with self._lock:
+                ok, out = self._call(v)
         if not ok:
             return http_error("network produced no output", 504)
         # json.NewEncoder(w).Encode(clientOutResponse{...}) (master.go:219): compact, newline-terminated
