@@ -119,6 +119,9 @@ def main():
     ap.add_argument("--gen-inputs", action="store_true",
                     help="diagnostic: generate inputs inside the executor instead of reading them from HBM")
     ap.add_argument("--graph", action="store_true", help="replay the timed launches as one captured HIP graph")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearse the multi-rank path on one GPU, with --dist-backend gloo)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -131,11 +134,16 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dist = None
+    if args.same_device:  # rehearsal of the N-rank path on a one-GPU box
+        local = 0
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
