@@ -2092,7 +2092,9 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (!sc->ok) why = sc->why;
     else {
         mk::JitShape shape;
-        if (mk::jit_lane_source(sc->prog, mk::JitLimits{}, lane, why, &shape))
+        mk::JitLimits lim;
+        if (const char *e = std::getenv("MK_JIT_MAX_DOPS")) lim.max_dops = (size_t)std::strtoull(e, nullptr, 10);
+        if (mk::jit_lane_source(sc->prog, lim, lane, why, &shape))
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape));
     }
     (void)mk::copy_out(out, out_len, why);

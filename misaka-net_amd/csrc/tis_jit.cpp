@@ -19,6 +19,7 @@
 //              lane that ends takes its next input while the others go on.
 #include "tis_jit.h"
 
+#include <algorithm>
 #include <cinttypes>
 #include <cstdarg>
 #include <cstdio>
@@ -234,13 +235,87 @@ struct OpWriter {
 
 // ---- stream shape: straight-line lane function ------------------------------
 
-void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e)
+// Longest path, in retired instructions, from variant 0 through fast
+// variants only (the guard never fires on it); the graph is acyclic here.
+uint64_t max_fast_steps(const SchedProgram &p, const Graph &g)
+{
+    std::vector<int64_t> memo(g.entry.size(), -1);
+    std::vector<uint32_t> stack{0u};
+    // iterative post-order DFS
+    std::vector<uint8_t> state(g.entry.size(), 0);
+    auto exits = [&](uint32_t v, std::vector<uint32_t> &succ) -> uint64_t {
+        succ.clear();
+        for (size_t pc = g.entry[v];; ++pc) {
+            const DOp &I = g.D[pc];
+            switch (I.op) {
+            case U_JUMP: succ.push_back((uint32_t)I.imm); return I.inc;
+            case U_BR:
+                succ.push_back((uint32_t)(uint64_t)I.imm);
+                succ.push_back((uint32_t)((uint64_t)I.imm >> 32));
+                return I.inc;
+            case U_JRO:
+                for (uint64_t t = 0; t <= I.b; ++t) succ.push_back(p.jtab[(size_t)I.imm + t]);
+                return I.inc;
+            case U_END: return I.inc;
+            default: break;
+            }
+        }
+    };
+    std::vector<uint32_t> succ;
+    while (!stack.empty()) {
+        const uint32_t v = stack.back();
+        if (state[v] == 0) {
+            state[v] = 1;
+            exits(v, succ);
+            for (uint32_t w : succ)
+                if (state[w] == 0) stack.push_back(w);
+            continue;
+        }
+        stack.pop_back();
+        if (state[v] == 2) continue;
+        const uint64_t inc = exits(v, succ);
+        int64_t best = 0;
+        for (uint32_t w : succ) best = std::max<int64_t>(best, memo[w]);
+        memo[v] = (int64_t)inc + best;
+        state[v] = 2;
+    }
+    return (uint64_t)memo[0];
+}
+
+// The lane function.  `unguarded`: the variant for launches whose budget
+// exceeds every path (max_fast_steps) -- no GUARD tests, no checked variants.
+void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const char *name, bool unguarded)
 {
     OpWriter w{e, p, "r"};
     const size_t nv = g.entry.size();
-    e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
-    e.line("#define MK_JIT_MACHINE 0");
-    e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
+    std::vector<char> live(nv, 0);
+    if (unguarded) {
+        std::deque<uint32_t> q{0};
+        live[0] = 1;
+        auto add = [&](uint32_t v) {
+            if (v < nv && !live[v]) {
+                live[v] = 1;
+                q.push_back(v);
+            }
+        };
+        while (!q.empty()) {
+            const uint32_t v = q.front();
+            q.pop_front();
+            for (size_t pc = g.entry[v];; ++pc) {
+                const DOp &I = g.D[pc];
+                if (I.op == U_JUMP) { add((uint32_t)I.imm); break; }
+                if (I.op == U_BR) { add((uint32_t)(uint64_t)I.imm); add((uint32_t)((uint64_t)I.imm >> 32)); break; }
+                if (I.op == U_JRO) {
+                    for (uint64_t t = 0; t <= I.b; ++t) add(p.jtab[(size_t)I.imm + t]);
+                    break;
+                }
+                if (I.op == U_END) break;
+            }
+        }
+    } else {
+        live = g.seen;
+    }
+    e.line("MK_FN int32_t %s(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,", name);
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
     e.line("{");
     for (uint32_t r = 0; r < p.nregs; ++r)
@@ -250,7 +325,7 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    int32_t outv = 0;");
     e.line("    (void)slots; (void)sstride; (void)budget;");
     for (uint32_t v = 0; v < nv; ++v) {
-        if (!g.seen[v]) continue;
+        if (!live[v]) continue;
         e.line("V%u:", v);
         for (size_t pc = g.entry[v];; ++pc) {
             const DOp &I = g.D[pc];
@@ -288,7 +363,8 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e)
                 e.line("    goto done;");
                 break;
             case U_GUARD:
-                e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", I.inc, (uint32_t)I.imm);
+                if (!unguarded)
+                    e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", I.inc, (uint32_t)I.imm);
                 leave = false;
                 break;
             case U_ROUND_END:
@@ -310,6 +386,17 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    *status_out = st;");
     e.line("    return outv;");
     e.line("}");
+}
+
+void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e)
+{
+    e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
+    e.line("#define MK_JIT_MACHINE 0");
+    // every path retires at most this many instructions: launches with a
+    // larger budget take the unguarded lane function
+    e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_fast_steps(p, g));
+    emit_stream_lane(p, g, e, "mk_lane", false);
+    emit_stream_lane(p, g, e, "mk_lane_ng", true);
 }
 
 // ---- machine shape: resumable lane --------------------------------------------
@@ -549,7 +636,7 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else
-        emit_stream_lane(p, g, e);
+        emit_stream(p, g, e);
     if (shape) *shape = s;
     src = std::move(e.s);
     return true;
@@ -574,7 +661,8 @@ __device__ __forceinline__ void mk_load4(const SParams &p, uint64_t base, int32_
     d = base + 3 < p.n ? sched_input(p, base + 3) : 0;
 }
 
-extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+template <bool NG>
+__device__ __forceinline__ void mk_stream_tiles(const SParams &p)
 {
     const uint32_t tid = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
@@ -589,10 +677,10 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
         const int32_t c0 = x0, c1 = x1, c2 = x2, c3 = x3;
         if (t + gridDim.x < ntiles) mk_load4(p, base + (uint64_t)gridDim.x * tile, x0, x1, x2, x3);
         uint32_t s0, s1, s2, s3, t0, t1, t2, t3;
-        int32_t o0 = mk_lane(c0, p.budget, slots, p.lanes, &s0, &t0);
-        int32_t o1 = mk_lane(c1, p.budget, slots, p.lanes, &s1, &t1);
-        int32_t o2 = mk_lane(c2, p.budget, slots, p.lanes, &s2, &t2);
-        int32_t o3 = mk_lane(c3, p.budget, slots, p.lanes, &s3, &t3);
+        int32_t o0 = (NG ? mk_lane_ng : mk_lane)(c0, p.budget, slots, p.lanes, &s0, &t0);
+        int32_t o1 = (NG ? mk_lane_ng : mk_lane)(c1, p.budget, slots, p.lanes, &s1, &t1);
+        int32_t o2 = (NG ? mk_lane_ng : mk_lane)(c2, p.budget, slots, p.lanes, &s2, &t2);
+        int32_t o3 = (NG ? mk_lane_ng : mk_lane)(c3, p.budget, slots, p.lanes, &s3, &t3);
         o0 = (t0 & MK_ST_HAS_OUTPUT) ? o0 : 0;
         o1 = (t1 & MK_ST_HAS_OUTPUT) ? o1 : 0;
         o2 = (t2 & MK_ST_HAS_OUTPUT) ? o2 : 0;
@@ -619,6 +707,14 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
         }
     }
     if (p.partials) write_partials(p.partials, gid, cnt);
+}
+
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    if ((uint64_t)p.budget > MK_MAX_STEPS)
+        mk_stream_tiles<true>(p); // the budget cannot be reached: no guards
+    else
+        mk_stream_tiles<false>(p);
 }
 )";
 

@@ -40,7 +40,12 @@ def build_lanes(cases, path):
             f"    std::vector<int32_t> slots({nslots} + 1, 0x5A5A5A5A);\n"
             f"    for (size_t i = 0; i < n; i++) {{\n"
             f"        uint32_t s, t;\n"
+            f"#if MK_JIT_MACHINE == 0\n"  # the kernel's dispatch: unguarded lane when no path reaches the budget
+            f"        const int32_t o = budget > MK_MAX_STEPS ? n{i}::mk_lane_ng(in[i], budget, slots.data(), 1, &s, &t)\n"
+            f"                                                : n{i}::mk_lane(in[i], budget, slots.data(), 1, &s, &t);\n"
+            f"#else\n"
             f"        const int32_t o = n{i}::mk_lane(in[i], budget, slots.data(), 1, &s, &t);\n"
+            f"#endif\n"
             f"        out[i] = (t & 0x10) ? o : 0; st[i] = (uint8_t)t; sp[i] = s;\n"
             f"    }}\n}}\n")
     src = path + ".cpp"
