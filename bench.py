@@ -42,8 +42,8 @@ WORKLOADS = {
     # name: (network factory, lanes per GPU, generator kind, mask, bytes per lane)
     "c2": ("c2_example_net_16M", mk.networks.example_network, 1 << 24, N.MK_GEN_FULL, 0),
     "c3": ("c3_sample_net_8M_per_gpu", mk.networks.sample_network, 1 << 23, N.MK_GEN_FULL, 0),
-    "c4": ("c4_pipeline_d64_64K", lambda: mk.networks.pipeline_network(64), 1 << 16, N.MK_GEN_FULL, 0),
-    "c4d1024": ("c4_pipeline_d1024_16K", lambda: mk.networks.pipeline_network(1024), 1 << 14, N.MK_GEN_FULL, 0),
+    "c4": ("c4_pipeline_d64_1M", lambda: mk.networks.pipeline_network(64), 1 << 20, N.MK_GEN_FULL, 0),
+    "c4d1024": ("c4_pipeline_d1024_256K", lambda: mk.networks.pipeline_network(1024), 1 << 18, N.MK_GEN_FULL, 0),
     "c5": ("c5_countdown_4M", mk.networks.countdown_network, 1 << 22, N.MK_GEN_MASKED, 1023),
 }
 

@@ -1086,6 +1086,9 @@ struct JitState {
     double compile_s = 0;
     size_t src_bytes = 0;
     JitShape shape = JIT_STREAM;
+    uint64_t max_steps = UINT64_MAX; // stream shape: launches need budget > max_steps
+    bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
+    int block = kJitBlock;
     JitDev dev[kMaxDevices];
 };
 
@@ -1433,8 +1436,10 @@ bool jit_compile(SchedCache *sc)
     const char *shp = std::getenv("MK_JIT_SHAPE"); // "machine" / "stream": force a shape (experiments)
     lim.force_machine = shp && std::strcmp(shp, "machine") == 0;
     lim.force_stream = shp && std::strcmp(shp, "stream") == 0;
-    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape)) return false;
-    const std::string src = jit_module_source(lane, J.shape);
+    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy)) return false;
+    J.heavy = J.heavy && J.shape == JIT_STREAM;
+    J.block = J.heavy ? kJitHeavyBlock : kJitBlock;
+    const std::string src = jit_module_source(lane, J.shape, J.heavy);
     J.src_bytes = src.size();
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
@@ -1474,7 +1479,7 @@ int ensure_jit_device(SchedCache *sc, int d)
     DeviceGuard g(d);
     if (hipModuleLoadData(&jd.mod, sc->jit.code.data()) != hipSuccess) return MK_EDEVICE;
     if (hipModuleGetFunction(&jd.fn, jd.mod, kJitKernel) != hipSuccess) return MK_EDEVICE;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, kJitBlock, 0) != hipSuccess ||
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, sc->jit.block, 0) != hipSuccess ||
         jd.per_cu < 1)
         jd.per_cu = 1;
     return MK_OK;
@@ -1503,11 +1508,12 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     JitDev &jd = sc->jit.dev[d];
     const SchedProgram &P = sc->prog;
     DeviceGuard g(d);
-    const uint64_t per_block = sc->jit.shape == JIT_STREAM ? (uint64_t)kJitBlock * kJitStreamLanes : kJitBlock;
+    const uint64_t block = (uint64_t)sc->jit.block;
+    const uint64_t per_block = sc->jit.shape == JIT_STREAM && !sc->jit.heavy ? block * kJitStreamLanes : block;
     const uint64_t want = (n + per_block - 1) / per_block;
     const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
-    const uint64_t lanes = (uint64_t)blocks * kJitBlock;
+    const uint64_t lanes = (uint64_t)blocks * block;
     if (P.nslots) {
         const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
         if (need > sd.slots_bytes) {
@@ -1543,7 +1549,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
                (uintptr_t)d_status % kJitStreamLanes == 0 && (uintptr_t)d_steps % va == 0;
     p.policy = jit_policy();
     void *args[] = {(void *)&p};
-    if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, kJitBlock, 1, 1, 0, stream, args, nullptr) != hipSuccess)
+    if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) != hipSuccess)
         return MK_EDEVICE;
     return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
@@ -1553,14 +1559,17 @@ enum Tier { TIER_NONE, TIER_INTERP, TIER_COMPILED, TIER_NATIVE };
 // Caller holds h->mu.  The tier a launch with `flags` runs on: tier 1 when
 // forced; else the native kernel unless tier 2 was asked for (TILE/REFILL);
 // else the superblock interpreter; tier 1 when the schedule compiler gave up.
-Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, SchedCache **out)
+// The stream-shaped native kernel has no budget checks: it serves launches
+// whose budget exceeds every path of the network; smaller budgets go to tier 2.
+Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, uint32_t budget, SchedCache **out)
 {
     *out = nullptr;
     if (flags & MK_FLAG_FORCE_INTERP) return TIER_INTERP;
     SchedCache *sc = get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
     *out = sc;
     const bool want_jit = (flags & MK_FLAG_JIT) || !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL));
-    if (want_jit && jit_compile(sc)) return TIER_NATIVE;
+    if (want_jit && jit_compile(sc) && (sc->jit.shape == JIT_MACHINE || (uint64_t)budget > sc->jit.max_steps))
+        return TIER_NATIVE;
     if (flags & MK_FLAG_JIT) return TIER_NONE;
     return sc->ok ? TIER_COMPILED : TIER_INTERP;
 }
@@ -1577,7 +1586,7 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     uint32_t budget, cap, flags;
     resolve_opts(o, budget, cap, flags);
     SchedCache *sc = nullptr;
-    switch (pick_tier(h, cap, flags, &sc)) {
+    switch (pick_tier(h, cap, flags, budget, &sc)) {
     case TIER_NATIVE:
         return launch_jit_locked(h, sc, d, in, n, d_out, d_status, d_steps, d_stats, budget, flags, stream);
     case TIER_COMPILED:
@@ -2033,13 +2042,15 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     char buf[1024];
     std::lock_guard<std::mutex> lk(h->mu);
     mk::SchedCache *sc = nullptr;
-    const mk::Tier t = mk::pick_tier(h, cap, flags, &sc);
+    const mk::Tier t = mk::pick_tier(h, cap, flags, budget, &sc);
     if (t == mk::TIER_INTERP) {
         snprintf(buf, sizeof buf, "tier=interp reason=%s", sc ? sc->why.c_str() : "forced");
         return mk::copy_out(out, out_len, buf);
     }
     if (t == mk::TIER_NONE) {
-        snprintf(buf, sizeof buf, "tier=none reason=native tier unavailable: %s", sc->jit.why.c_str());
+        snprintf(buf, sizeof buf, "tier=none reason=native tier unavailable: %s",
+                 sc->jit.ok ? "budget within the network's longest path (the native stream kernel has no budget checks)"
+                            : sc->jit.why.c_str());
         (void)mk::copy_out(out, out_len, buf);
         return MK_ELIMIT;
     }
@@ -2050,7 +2061,8 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (t == mk::TIER_NATIVE) {
         char tail[160];
         snprintf(tail, sizeof tail, " shape=%s source=%zuB code=%zuB compile=%.2fs",
-                 sc->jit.shape == mk::JIT_MACHINE ? "machine" : "stream", sc->jit.src_bytes, sc->jit.code.size(),
+                 sc->jit.shape == mk::JIT_MACHINE ? "machine" : sc->jit.heavy ? "stream-heavy" : "stream",
+                 sc->jit.src_bytes, sc->jit.code.size(),
                  sc->jit.compile_s);
         s = std::string("tier=native ") + buf + tail;
     } else {
@@ -2058,7 +2070,9 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         uint32_t B, K;
         mk::sched_geometry(P.nregs, B, K);
         snprintf(buf + len, sizeof buf - len, " lanes=%s K=%u B=%u native=%s", tile ? "tile" : "refill", K, B,
-                 sc->jit.tried ? (sc->jit.ok ? "ok" : sc->jit.why.c_str()) : "not-requested");
+                 !sc->jit.tried ? "not-requested"
+                 : !sc->jit.ok  ? sc->jit.why.c_str()
+                                : "ok-but-budget-within-longest-path");
         s = std::string("tier=compiled ") + buf;
     }
     return mk::copy_out(out, out_len, s);
@@ -2073,7 +2087,7 @@ int mk_net_prepare(mk_net *h, const mk_opts *opts, int device)
     int rc = mk::ensure_device(h, device);
     if (rc) return rc;
     mk::SchedCache *sc = nullptr;
-    switch (mk::pick_tier(h, cap, flags, &sc)) {
+    switch (mk::pick_tier(h, cap, flags, budget, &sc)) {
     case mk::TIER_NATIVE: return mk::ensure_jit_device(sc, device);
     case mk::TIER_COMPILED: return mk::ensure_sched_device(sc, device);
     case mk::TIER_NONE: return MK_ELIMIT;
@@ -2094,8 +2108,9 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         mk::JitShape shape;
         mk::JitLimits lim;
         if (const char *e = std::getenv("MK_JIT_MAX_DOPS")) lim.max_dops = (size_t)std::strtoull(e, nullptr, 10);
-        if (mk::jit_lane_source(sc->prog, lim, lane, why, &shape))
-            return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape));
+        bool heavy = false;
+        if (mk::jit_lane_source(sc->prog, lim, lane, why, &shape, nullptr, &heavy))
+            return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM));
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

@@ -59,15 +59,123 @@ std::string u64lit(int64_t v)
     return b;
 }
 
+// A stretch of a superblock that repeats: `reps` copies of `period`
+// micro-ops that are identical except for stack-slot numbers (ST/LD/STI)
+// and round-end step counts (ROUND_END), which advance by a fixed amount
+// per copy.  The schedule compiler unrolls every loop whose control is
+// constant (a PUSH loop of 64: 64 copies of its body, one slot apart); the
+// generator rolls such stretches back into `for` loops, which keeps the
+// source small enough for hiprtc (a straight-line 23K-op lane takes minutes
+// to compile) at the cost of an index computation per slot access.
+struct Run {
+    size_t start = 0, period = 0, reps = 0;
+    std::vector<int64_t> delta; // per op of the period: slot or step advance per copy
+    std::vector<Run> inner;     // runs inside the first copy (nested loops)
+};
+
 // The reachable part of a schedule's device form.
 struct Graph {
     std::vector<DOp> D;
     std::vector<uint32_t> entry;
     std::vector<char> seen;      // variant reachable from variant 0
     std::vector<char> used_reg;  // register read or written by reachable code
-    size_t nreach = 0, ndops = 0;
+    size_t nreach = 0, ndops = 0; // ndops: micro-ops emitted (rolled runs count once)
     bool cyclic = false;
+    std::vector<std::vector<Run>> runs; // per variant, ascending start
 };
+
+bool slot_op(const DOp &I) { return I.op == U_ST || I.op == U_LD || I.op == U_STI; }
+
+// The advancing field of an op: slot for ST/LD (imm) and STI (d), step count
+// for ROUND_END (inc); -1 for ops without one.
+int64_t advancing(const DOp &I)
+{
+    if (I.op == U_ST || I.op == U_LD) return (int64_t)(uint32_t)I.imm;
+    if (I.op == U_STI) return I.d;
+    if (I.op == U_ROUND_END) return I.inc;
+    return -1;
+}
+
+// Equal apart from the advancing field.
+bool same_shape(const DOp &x, const DOp &y)
+{
+    if (x.op != y.op || x.fl != y.fl || x.a != y.a || x.b != y.b) return false;
+    switch (x.op) {
+    case U_ST: case U_LD: return x.d == y.d;
+    case U_STI: return x.imm == y.imm;
+    case U_ROUND_END: return x.d == y.d && x.imm == y.imm;
+    default: return x.d == y.d && x.imm == y.imm && x.inc == y.inc;
+    }
+}
+
+constexpr size_t kRunMaxPeriod = 512, kRunMinReps = 3, kRunMinOps = 24;
+
+// Greedy roll-up of the body [lo, hi) of one variant (data ops and ROUND_END),
+// nested: each run's first copy is rolled again.  `outer` are the enclosing
+// runs: an op inside a run must advance by the same amount per enclosing
+// copy in every copy of the run, so that one affine expression covers it.
+std::vector<Run> find_runs(const std::vector<DOp> &D, size_t lo, size_t hi, std::vector<const Run *> &outer)
+{
+    auto same_outer = [&](size_t a, size_t b) {
+        for (const Run *o : outer)
+            if (o->delta[a - o->start] != o->delta[b - o->start]) return false;
+        return true;
+    };
+    std::vector<Run> out;
+    size_t i = lo;
+    while (i < hi) {
+        Run best;
+        const size_t pmax = std::min(kRunMaxPeriod, (hi - i) / kRunMinReps);
+        for (size_t P = 1; P <= pmax; ++P) {
+            if (!same_shape(D[i], D[i + P])) continue;
+            // deltas from the first two copies
+            std::vector<int64_t> dl(P);
+            bool ok = true;
+            for (size_t k = 0; k < P && ok; ++k) {
+                const DOp &x = D[i + k], &y = D[i + P + k];
+                ok = same_shape(x, y) && same_outer(i + k, i + P + k);
+                const int64_t ax = advancing(x), ay = advancing(y);
+                dl[k] = ax >= 0 ? ay - ax : 0;
+            }
+            if (!ok) continue;
+            size_t r = 2;
+            for (;; ++r) {
+                if (i + (r + 1) * P > hi) break;
+                bool m = true;
+                for (size_t k = 0; k < P && m; ++k) {
+                    const DOp &x = D[i + k], &y = D[i + r * P + k];
+                    m = same_shape(x, y) && same_outer(i + k, i + r * P + k) &&
+                        (advancing(x) < 0 || advancing(y) == advancing(x) + (int64_t)r * dl[k]);
+                }
+                if (!m) break;
+            }
+            if (r >= kRunMinReps && r * P >= kRunMinOps && r * P > best.reps * best.period) {
+                best.start = i;
+                best.period = P;
+                best.reps = r;
+                best.delta = dl;
+            }
+        }
+        if (best.reps) {
+            outer.push_back(&best);
+            best.inner = find_runs(D, best.start, best.start + best.period, outer);
+            outer.pop_back();
+            i += best.reps * best.period;
+            out.push_back(std::move(best));
+        } else {
+            ++i;
+        }
+    }
+    return out;
+}
+
+// Micro-ops emitted for [lo, hi) with `runs` rolled.
+size_t emitted_ops(const std::vector<Run> &runs, size_t lo, size_t hi)
+{
+    size_t n = hi - lo;
+    for (const Run &r : runs) n = n - r.reps * r.period + emitted_ops(r.inner, r.start, r.start + r.period);
+    return n;
+}
 
 bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string &why)
 {
@@ -104,7 +212,7 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
                 why = "superblock runs off the code";
                 return false;
             }
-            if (++g.ndops > lim.max_dops) {
+            if (++g.ndops > lim.max_scan) {
                 why = "schedule too large for the native tier";
                 return false;
             }
@@ -150,6 +258,37 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
             why = "register out of range";
             return false;
         }
+    // roll repeating stretches; the emitted size is what the limit applies to
+    // (acyclic: the GPU kernel holds only the variants reachable without
+    // taking a guard -- see emit_stream)
+    std::vector<char> counted = g.seen;
+    if (!g.cyclic) {
+        counted.assign(nv, 0);
+        std::deque<uint32_t> q{0};
+        counted[0] = 1;
+        while (!q.empty()) {
+            const uint32_t v = q.front();
+            q.pop_front();
+            for (uint32_t w : succ[v])
+                if (!(v & 1u) && w == v + 1 && g.D[g.entry[v]].op == U_GUARD) continue; // the guard edge
+                else if (!counted[w]) counted[w] = 1, q.push_back(w);
+        }
+    }
+    g.runs.assign(nv, {});
+    g.ndops = 0;
+    for (uint32_t v = 0; v < nv; ++v) {
+        if (!g.seen[v]) continue;
+        size_t lo = g.entry[v], hi = lo;
+        if (g.D[lo].op == U_GUARD) ++lo, ++hi;
+        while (g.D[hi].op <= U_LD || g.D[hi].op == U_ROUND_END) ++hi;
+        std::vector<const Run *> outer;
+        g.runs[v] = find_runs(g.D, lo, hi, outer);
+        if (counted[v]) g.ndops += (lo - g.entry[v]) + emitted_ops(g.runs[v], lo, hi) + 1;
+    }
+    if (g.ndops > lim.max_dops) {
+        why = "schedule too large for the native tier";
+        return false;
+    }
     // cycle detection over reachable variants (iterative DFS, colours 0/1/2)
     std::vector<uint8_t> col(nv, 0);
     std::vector<std::pair<uint32_t, size_t>> st{{0u, 0}};
@@ -203,11 +342,17 @@ struct OpWriter {
         return "(" + operand(I.a, I.fl & UF_TA) + " " + cmp[(I.fl >> UF_COND_SHIFT) & 3u] + ")";
     }
 
-    // Data micro-ops; returns false for an exit / control op.
-    bool data(const DOp &I) const
+    // Data micro-ops; returns false for an exit / control op.  `slot`
+    // overrides the slot number of ST/LD/STI (an expression in a rolled loop).
+    bool data(const DOp &I, const char *slot = nullptr) const
     {
         const std::string A = operand(I.a, I.fl & UF_TA), B = operand(I.b, I.fl & UF_TB);
         const uint32_t d = I.d / 8;
+        char sb[64];
+        if (!slot) {
+            snprintf(sb, sizeof sb, "%uu", I.op == U_STI ? I.d : (uint32_t)I.imm);
+            slot = sb;
+        }
         switch (I.op) {
         case U_MOV: e.line("    %s%u = %s;", R, d, A.c_str()); return true;
         case U_LI: e.line("    %s%u = (int64_t)%s;", R, d, u64lit(I.imm).c_str()); return true;
@@ -215,11 +360,11 @@ struct OpWriter {
         case U_SUB: e.line("    %s%u = (int64_t)((uint64_t)%s - (uint64_t)%s);", R, d, A.c_str(), B.c_str()); return true;
         case U_ADDI: e.line("    %s%u = (int64_t)((uint64_t)%s + %s);", R, d, A.c_str(), u64lit(I.imm).c_str()); return true;
         case U_RSUBI: e.line("    %s%u = (int64_t)(%s - (uint64_t)%s);", R, d, u64lit(I.imm).c_str(), A.c_str()); return true;
-        case U_ST: e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%s;", (uint32_t)I.imm, A.c_str()); return true;
+        case U_ST: e.line("    slots[(uint64_t)(%s) * sstride] = (int32_t)%s;", slot, A.c_str()); return true;
         case U_STI:
-            e.line("    slots[(uint64_t)%uu * sstride] = (int32_t)%" PRId32 ";", I.d, (int32_t)I.imm);
+            e.line("    slots[(uint64_t)(%s) * sstride] = (int32_t)%" PRId32 ";", slot, (int32_t)I.imm);
             return true;
-        case U_LD: e.line("    %s%u = (int64_t)slots[(uint64_t)%uu * sstride];", R, d, (uint32_t)I.imm); return true;
+        case U_LD: e.line("    %s%u = (int64_t)slots[(uint64_t)(%s) * sstride];", R, d, slot); return true;
         default: return false;
         }
     }
@@ -232,6 +377,64 @@ struct OpWriter {
         e.line("        t = t < 0 ? 0 : t;");
     }
 };
+
+// Emits the body [lo, hi) of a variant -- data ops and ROUND_END markers --
+// rolling `runs` into nested for loops (loop variables j0, j1, ...); an
+// op's slot or step count is its value in the first copy plus, per
+// enclosing loop, that loop's variable times the op's advance.
+// `round_end(I, inc)` prints a ROUND_END whose step count is the expression `inc`.
+template <class RoundEnd>
+void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs, size_t lo, size_t hi,
+                 std::vector<const Run *> &outer, RoundEnd &round_end)
+{
+    size_t ri = 0;
+    auto expr = [&](size_t pc, int64_t base) {
+        std::string x = std::to_string(base) + "ll";
+        for (size_t L = 0; L < outer.size(); ++L) {
+            const int64_t d = outer[L]->delta[pc - outer[L]->start];
+            if (d) x += " + (int64_t)j" + std::to_string(L) + " * " + std::to_string(d) + "ll";
+        }
+        return x;
+    };
+    for (size_t pc = lo; pc < hi;) {
+        if (ri < runs.size() && runs[ri].start == pc) {
+            const Run &r = runs[ri++];
+            w.e.line("    for (uint32_t j%zu = 0; j%zu < %zuu; ++j%zu) {", outer.size(), outer.size(), r.reps,
+                     outer.size());
+            outer.push_back(&r);
+            emit_rolled(w, g, r.inner, r.start, r.start + r.period, outer, round_end);
+            outer.pop_back();
+            w.e.line("    }");
+            pc += r.reps * r.period;
+            continue;
+        }
+        const DOp &I = g.D[pc];
+        if (slot_op(I)) {
+            w.data(I, expr(pc, advancing(I)).c_str());
+        } else if (I.op == U_ROUND_END) {
+            round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+        } else {
+            w.data(I);
+        }
+        ++pc;
+    }
+}
+
+template <class RoundEnd>
+void emit_body(const OpWriter &w, const Graph &g, uint32_t v, size_t lo, size_t hi, RoundEnd round_end)
+{
+    std::vector<const Run *> outer;
+    emit_rolled(w, g, g.runs[v], lo, hi, outer, round_end);
+}
+
+// [lo, hi) of variant v's body: after its GUARD, up to its exit op.
+void body_range(const Graph &g, uint32_t v, size_t &lo, size_t &hi)
+{
+    lo = g.entry[v];
+    if (g.D[lo].op == U_GUARD) ++lo;
+    hi = lo;
+    while (g.D[hi].op <= U_LD || g.D[hi].op == U_ROUND_END) ++hi;
+}
 
 // ---- stream shape: straight-line lane function ------------------------------
 
@@ -327,58 +530,52 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
     for (uint32_t v = 0; v < nv; ++v) {
         if (!live[v]) continue;
         e.line("V%u:", v);
-        for (size_t pc = g.entry[v];; ++pc) {
-            const DOp &I = g.D[pc];
-            if (w.data(I)) continue;
-            bool leave = true;
-            switch (I.op) {
-            case U_JUMP:
-                e.line("    steps += %uu;", I.inc);
-                e.line("    goto V%u;", (uint32_t)I.imm);
-                break;
-            case U_BR:
-                e.line("    steps += %uu;", I.inc);
-                e.line("    if %s goto V%u;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm);
-                e.line("    goto V%u;", (uint32_t)((uint64_t)I.imm >> 32));
-                break;
-            case U_JRO: {
-                e.line("    steps += %uu;", I.inc);
-                e.line("    {");
-                w.jro_target(I);
-                e.line("        switch (t) {");
-                const uint32_t last = p.jtab[(size_t)I.imm + I.b];
-                for (uint32_t t = 0; t < I.b; ++t) {
-                    const uint32_t tgt = p.jtab[(size_t)I.imm + t];
-                    if (tgt != last) e.line("        case %u: goto V%u;", t, tgt);
-                }
-                e.line("        default: goto V%u;", last);
-                e.line("        }");
-                e.line("    }");
-                break;
+        const DOp &G = g.D[g.entry[v]];
+        if (G.op == U_GUARD && !unguarded)
+            e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", G.inc, (uint32_t)G.imm);
+        size_t lo, hi;
+        body_range(g, v, lo, hi);
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc) {
+            e.line("    if ((uint64_t)steps + %s >= (uint64_t)budget) {", inc);
+            e.line("        steps += (uint32_t)(%s);", inc);
+            e.line("        outv = %s;", w.result(I).c_str());
+            e.line("        st = %uu;", I.d);
+            e.line("        goto done;");
+            e.line("    }");
+        });
+        const DOp &I = g.D[hi];
+        switch (I.op) {
+        case U_JUMP:
+            e.line("    steps += %uu;", I.inc);
+            e.line("    goto V%u;", (uint32_t)I.imm);
+            break;
+        case U_BR:
+            e.line("    steps += %uu;", I.inc);
+            e.line("    if %s goto V%u;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm);
+            e.line("    goto V%u;", (uint32_t)((uint64_t)I.imm >> 32));
+            break;
+        case U_JRO: {
+            e.line("    steps += %uu;", I.inc);
+            e.line("    {");
+            w.jro_target(I);
+            e.line("        switch (t) {");
+            const uint32_t last = p.jtab[(size_t)I.imm + I.b];
+            for (uint32_t t = 0; t < I.b; ++t) {
+                const uint32_t tgt = p.jtab[(size_t)I.imm + t];
+                if (tgt != last) e.line("        case %u: goto V%u;", t, tgt);
             }
-            case U_END:
-                e.line("    steps += %uu;", I.inc);
-                e.line("    outv = %s;", w.result(I).c_str());
-                e.line("    st = %uu;", I.d);
-                e.line("    goto done;");
-                break;
-            case U_GUARD:
-                if (!unguarded)
-                    e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", I.inc, (uint32_t)I.imm);
-                leave = false;
-                break;
-            case U_ROUND_END:
-                e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) {", I.inc);
-                e.line("        steps += %uu;", I.inc);
-                e.line("        outv = %s;", w.result(I).c_str());
-                e.line("        st = %uu;", I.d);
-                e.line("        goto done;");
-                e.line("    }");
-                leave = false;
-                break;
-            default: break;
-            }
-            if (leave) break;
+            e.line("        default: goto V%u;", last);
+            e.line("        }");
+            e.line("    }");
+            break;
+        }
+        case U_END:
+            e.line("    steps += %uu;", I.inc);
+            e.line("    outv = %s;", w.result(I).c_str());
+            e.line("    st = %uu;", I.d);
+            e.line("    goto done;");
+            break;
+        default: break;
         }
     }
     e.line("done:");
@@ -388,14 +585,18 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
     e.line("}");
 }
 
-void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e)
+// The kernel runs only launches whose budget exceeds every path
+// (MK_MAX_STEPS): its lane function has no guards and no checked variants.
+// The guarded lane (MK_LANE_CHECKED) is for the CPU tests; the executor
+// gives launches with a smaller budget to tier 2.
+void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps)
 {
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 0");
-    // every path retires at most this many instructions: launches with a
-    // larger budget take the unguarded lane function
-    e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_fast_steps(p, g));
+    e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_steps);
+    e.line("#ifdef MK_LANE_CHECKED");
     emit_stream_lane(p, g, e, "mk_lane", false);
+    e.line("#endif");
     emit_stream_lane(p, g, e, "mk_lane_ng", true);
 }
 
@@ -547,64 +748,62 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             emit_self_loop(w, g, v, gpc, xpc);
             continue;
         }
-        for (size_t pc = g.entry[v];; ++pc) {
-            const DOp &I = g.D[pc];
-            if (w.data(I)) continue;
-            bool leave = true;
-            switch (I.op) {
-            case U_JUMP:
-                e.line("    L.steps += %uu;", I.inc);
-                e.line("    L.sb = %uu;", (uint32_t)I.imm);
-                break;
-            case U_BR:
-                e.line("    L.steps += %uu;", I.inc);
-                e.line("    L.sb = %s ? %uu : %uu;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm,
-                       (uint32_t)((uint64_t)I.imm >> 32));
-                break;
-            case U_JRO: {
-                e.line("    L.steps += %uu;", I.inc);
-                e.line("    {");
-                w.jro_target(I);
-                const uint32_t last = p.jtab[(size_t)I.imm + I.b];
-                std::string sel;
-                for (uint32_t t = 0; t < I.b; ++t) {
-                    const uint32_t tgt = p.jtab[(size_t)I.imm + t];
-                    if (tgt == last) continue;
-                    char b[64];
-                    snprintf(b, sizeof b, "t == %u ? %uu : ", t, tgt);
-                    sel += b;
-                }
-                e.line("        L.sb = %s%uu;", sel.c_str(), last);
-                e.line("    }");
-                break;
-            }
-            case U_END:
-                e.line("    L.steps += %uu;", I.inc);
-                e.line("    L.outv = %s;", w.result(I).c_str());
-                e.line("    L.st = %uu;", I.d);
-                e.line("    L.sb = MK_SB_DONE;");
-                break;
-            case U_GUARD:
-                e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", I.inc);
-                e.line("        L.sb = %uu;", (uint32_t)I.imm);
-                e.line("        break;");
-                e.line("    }");
-                leave = false;
-                break;
-            case U_ROUND_END:
-                e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", I.inc);
-                e.line("        L.steps += %uu;", I.inc);
-                e.line("        L.outv = %s;", w.result(I).c_str());
-                e.line("        L.st = %uu;", I.d);
-                e.line("        L.sb = MK_SB_DONE;");
-                e.line("        break;");
-                e.line("    }");
-                leave = false;
-                break;
-            default: break;
-            }
-            if (leave) break;
+        // early exits jump to X<v>, the end of the case
+        const DOp &G = g.D[g.entry[v]];
+        if (G.op == U_GUARD) {
+            e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", G.inc);
+            e.line("        L.sb = %uu;", (uint32_t)G.imm);
+            e.line("        goto X%u;", v);
+            e.line("    }");
         }
+        size_t lo, hi;
+        body_range(g, v, lo, hi);
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc) {
+            e.line("    if ((uint64_t)L.steps + %s >= (uint64_t)budget) {", inc);
+            e.line("        L.steps += (uint32_t)(%s);", inc);
+            e.line("        L.outv = %s;", w.result(I).c_str());
+            e.line("        L.st = %uu;", I.d);
+            e.line("        L.sb = MK_SB_DONE;");
+            e.line("        goto X%u;", v);
+            e.line("    }");
+        });
+        const DOp &I = g.D[hi];
+        switch (I.op) {
+        case U_JUMP:
+            e.line("    L.steps += %uu;", I.inc);
+            e.line("    L.sb = %uu;", (uint32_t)I.imm);
+            break;
+        case U_BR:
+            e.line("    L.steps += %uu;", I.inc);
+            e.line("    L.sb = %s ? %uu : %uu;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm,
+                   (uint32_t)((uint64_t)I.imm >> 32));
+            break;
+        case U_JRO: {
+            e.line("    L.steps += %uu;", I.inc);
+            e.line("    {");
+            w.jro_target(I);
+            const uint32_t last = p.jtab[(size_t)I.imm + I.b];
+            std::string sel;
+            for (uint32_t t = 0; t < I.b; ++t) {
+                const uint32_t tgt = p.jtab[(size_t)I.imm + t];
+                if (tgt == last) continue;
+                char b[64];
+                snprintf(b, sizeof b, "t == %u ? %uu : ", t, tgt);
+                sel += b;
+            }
+            e.line("        L.sb = %s%uu;", sel.c_str(), last);
+            e.line("    }");
+            break;
+        }
+        case U_END:
+            e.line("    L.steps += %uu;", I.inc);
+            e.line("    L.outv = %s;", w.result(I).c_str());
+            e.line("    L.st = %uu;", I.d);
+            e.line("    L.sb = MK_SB_DONE;");
+            break;
+        default: break;
+        }
+        e.line("    X%u:", v);
         e.line("    break;");
         e.line("    }");
     }
@@ -627,7 +826,8 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 
 } // namespace
 
-bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape)
+bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
+                     uint64_t *max_steps, bool *heavy)
 {
     Graph g;
     if (!analyze(p, lim, g, why)) return false;
@@ -636,8 +836,10 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else
-        emit_stream(p, g, e);
+        emit_stream(p, g, e, max_fast_steps(p, g));
     if (shape) *shape = s;
+    if (max_steps) *max_steps = s == JIT_STREAM ? max_fast_steps(p, g) : UINT64_MAX;
+    if (heavy) *heavy = g.ndops > kJitHeavyOps;
     src = std::move(e.s);
     return true;
 }
@@ -661,8 +863,7 @@ __device__ __forceinline__ void mk_load4(const SParams &p, uint64_t base, int32_
     d = base + 3 < p.n ? sched_input(p, base + 3) : 0;
 }
 
-template <bool NG>
-__device__ __forceinline__ void mk_stream_tiles(const SParams &p)
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 {
     const uint32_t tid = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
@@ -677,10 +878,10 @@ __device__ __forceinline__ void mk_stream_tiles(const SParams &p)
         const int32_t c0 = x0, c1 = x1, c2 = x2, c3 = x3;
         if (t + gridDim.x < ntiles) mk_load4(p, base + (uint64_t)gridDim.x * tile, x0, x1, x2, x3);
         uint32_t s0, s1, s2, s3, t0, t1, t2, t3;
-        int32_t o0 = (NG ? mk_lane_ng : mk_lane)(c0, p.budget, slots, p.lanes, &s0, &t0);
-        int32_t o1 = (NG ? mk_lane_ng : mk_lane)(c1, p.budget, slots, p.lanes, &s1, &t1);
-        int32_t o2 = (NG ? mk_lane_ng : mk_lane)(c2, p.budget, slots, p.lanes, &s2, &t2);
-        int32_t o3 = (NG ? mk_lane_ng : mk_lane)(c3, p.budget, slots, p.lanes, &s3, &t3);
+        int32_t o0 = mk_lane_ng(c0, p.budget, slots, p.lanes, &s0, &t0);
+        int32_t o1 = mk_lane_ng(c1, p.budget, slots, p.lanes, &s1, &t1);
+        int32_t o2 = mk_lane_ng(c2, p.budget, slots, p.lanes, &s2, &t2);
+        int32_t o3 = mk_lane_ng(c3, p.budget, slots, p.lanes, &s3, &t3);
         o0 = (t0 & MK_ST_HAS_OUTPUT) ? o0 : 0;
         o1 = (t1 & MK_ST_HAS_OUTPUT) ? o1 : 0;
         o2 = (t2 & MK_ST_HAS_OUTPUT) ? o2 : 0;
@@ -709,12 +910,32 @@ __device__ __forceinline__ void mk_stream_tiles(const SParams &p)
     if (p.partials) write_partials(p.partials, gid, cnt);
 }
 
+)";
+
+// Kernel of the stream shape for heavy lanes (more than kJitHeavyOps
+// micro-ops: long programs, deep stacks): one lane per thread, grid-stride,
+// small blocks so that modest batches still spread over every CU, and one
+// copy of the lane code (hiprtc time grows with it).
+static const char *const kStreamKernelHeavy = R"(
 extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 {
-    if ((uint64_t)p.budget > MK_MAX_STEPS)
-        mk_stream_tiles<true>(p); // the budget cannot be reached: no guards
-    else
-        mk_stream_tiles<false>(p);
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    uint64_t i = gid;
+    int32_t cur = i < p.n ? sched_input(p, i) : 0;
+    for (; i < p.n; i += stride) {
+        const int32_t nxt = i + stride < p.n ? sched_input(p, i + stride) : 0;
+        uint32_t s, t;
+        const int32_t o = mk_lane_ng(cur, p.budget, slots, p.lanes, &s, &t);
+        p.out[i] = (t & MK_ST_HAS_OUTPUT) ? o : 0;
+        p.status[i] = (uint8_t)t;
+        if (p.steps) p.steps[i] = s;
+        count_lane(cnt, s, t);
+        cur = nxt;
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
 }
 )";
 
@@ -775,7 +996,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 }
 )";
 
-std::string jit_module_source(const std::string &lane_src, JitShape shape)
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy)
 {
     Emitter e;
     // hiprtc declares the fixed-width integer types in __hip_internal only
@@ -814,7 +1035,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape)
     e.s += kDeviceCommon;
     e.s += "\n";
     e.s += lane_src;
-    e.s += shape == JIT_MACHINE ? kMachineKernel : kStreamKernel;
+    e.s += shape == JIT_MACHINE ? kMachineKernel : heavy ? kStreamKernelHeavy : kStreamKernel;
     return e.s;
 }
 

@@ -24,8 +24,10 @@ namespace mk {
 
 struct JitLimits {
     uint32_t max_variants = 4096; // superblock variants (labels)
-    size_t max_dops = 4096;       // micro-ops in the reachable code (hiprtc time grows
-                                  // superlinearly: 14K straight-line ops take ~150 s)
+    size_t max_dops = 4096;       // micro-ops emitted, after rolling repeats into loops
+                                  // (hiprtc time grows superlinearly: 14K straight-line
+                                  // ops take ~150 s)
+    size_t max_scan = 1u << 22;   // micro-ops of reachable code scanned before giving up
     bool force_machine = false;   // machine shape even for acyclic graphs (tests)
     bool force_stream = false;    // stream shape even for cyclic graphs (experiments)
 };
@@ -40,18 +42,24 @@ enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
 // MK_KEEP which the includer defines).  `slots` points at stack slot 0 of the
 // lane, slot s at slots[s * sstride].  MK_FN is defined by the includer.
 // Returns false (why) when over limits.
+// max_steps: the stream shape's longest path in retired instructions (its
+// kernel serves launches with a larger budget only); UINT64_MAX for machine.
+// heavy: more than kJitHeavyOps micro-ops emitted (the stream shape then
+// runs one lane per thread in 64-thread blocks instead of 4-lane tiles).
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why,
-                     JitShape *shape = nullptr);
+                     JitShape *shape = nullptr, uint64_t *max_steps = nullptr, bool *heavy = nullptr);
 
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of
 // the given shape.
-std::string jit_module_source(const std::string &lane_src, JitShape shape);
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy = false);
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
+constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane per thread
+constexpr int kJitHeavyBlock = 64;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.

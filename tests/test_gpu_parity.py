@@ -47,7 +47,7 @@ def test_readme_kat_on_gpu(gpu):
 # "auto": the default path (the native per-network kernel when the schedule
 # fits its limits, else tier 2); tier 2 with both lane schedulings; tier 1
 MODES = ["auto", "tile", "refill", "interp"]
-NATIVE = {"c2_example", "c3_sample", "c5_countdown"}  # configs whose default path is the native tier
+NATIVE = {"c2_example", "c3_sample", "c4_pipeline_d64", "c5_countdown"}  # default path: the native tier
 
 
 @pytest.mark.parametrize("mode", MODES)
