@@ -629,32 +629,50 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
 // Self-loop v as a wave-uniform loop with per-lane predication.  The lanes
 // of the group run the body together; a lane's flag `a` drops once it leaves
 // the loop (branch not taken, or the next iteration's budget guard fails) and
-// from then on its registers and steps stay frozen (selects), so the loop
-// control is scalar and no divergent branch or exec-mask bookkeeping is paid
-// per iteration -- only the body, the selects and two compares.  The wave
-// checks every MK_UNROLL iterations whether enough of the group is still in
-// the loop (MK_KEEP), so a few long trips do not hold the others.
+// from then on its registers stay frozen (selects), so the loop control is
+// scalar and no divergent branch or exec-mask bookkeeping is paid per
+// iteration.  The wave checks every kLoopUnroll iterations whether enough of
+// the group is still in the loop (MK_KEEP), so a few long trips do not hold
+// the others.
+//
+// Two phases.  At entry the wave has the largest step count of its lanes
+// (smax, from the dispatcher) and from it the number of iterations T that no lane's budget
+// guard can stop; those run unguarded and without step counting -- a lane's
+// steps are recovered at the end from its trip count, read off an induction
+// register (a register the body only bumps by a constant, whose bump is
+// predicated instead of selected) or, without one, a per-lane counter.  Only
+// iterations past T (a launch whose budget ends inside the loop) run the
+// guarded body, which keeps steps exact per iteration.
 constexpr int kLoopUnroll = 4;
 
 void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
 {
     Emitter &e = w.e;
     const DOp &G = g.D[gpc], &X = g.D[xpc];
-    // registers the body reads or writes, and the ones it writes
-    std::vector<char> rd(g.used_reg.size(), 0), wr(g.used_reg.size(), 0);
+    // registers the body reads or writes, the ones it writes, and how often
+    const size_t nr = g.used_reg.size();
+    std::vector<char> rd(nr, 0), wr(nr, 0);
+    std::vector<int> nwr(nr, 0);
     auto R = [&](uint32_t off) { rd[off / 8] = 1; };
-    auto W = [&](uint32_t off) { wr[off / 8] = rd[off / 8] = 1; };
-    bool stores = false;
+    auto W = [&](uint32_t off) { wr[off / 8] = rd[off / 8] = 1; ++nwr[off / 8]; };
     for (size_t pc = gpc + 1; pc < xpc; ++pc) {
         const DOp &I = g.D[pc];
         switch (I.op) {
         case U_MOV: case U_ADDI: case U_RSUBI: R(I.a); W(I.d); break;
         case U_ADD: case U_SUB: R(I.a); R(I.b); W(I.d); break;
         case U_LI: case U_LD: W(I.d); break;
-        case U_ST: R(I.a); stores = true; break;
-        case U_STI: stores = true; break;
+        case U_ST: R(I.a); break;
         default: break;
         }
+    }
+    // induction register: written once per iteration, by r += imm (no truncation)
+    int ind = -1;
+    int64_t step = 0;
+    for (size_t pc = gpc + 1; pc < xpc && ind < 0; ++pc) {
+        const DOp &I = g.D[pc];
+        if (I.op == U_ADDI && I.a == I.d && !(I.fl & UF_TA) && nwr[I.d / 8] == 1 && I.imm != 0 &&
+            I.imm > -(int64_t(1) << 31) && I.imm < (int64_t(1) << 31))
+            ind = (int)(I.d / 8), step = I.imm;
     }
     std::string c = "true";
     uint32_t other = v;
@@ -665,6 +683,34 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         if (tk == v && nt != v) c = n.cond(X), other = nt;
         else if (tk != v) c = "!" + n.cond(X), other = tk;
     }
+    // one iteration; guarded: steps counted and the budget checked per iteration
+    auto iteration = [&](bool guarded) {
+        e.line("    {");
+        for (uint32_t r = 0; r < nr; ++r)
+            if (rd[r]) e.line("    int64_t n%u = L.r%u;", r, r);
+        OpWriter n{e, w.p, "n"};
+        for (size_t pc = gpc + 1; pc < xpc; ++pc) {
+            const DOp &I = g.D[pc];
+            if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
+            if (I.op == U_ADDI && (int)(I.d / 8) == ind)
+                e.line("    n%d = (int64_t)((uint64_t)n%d + (a ? %s : 0ull));", ind, ind, u64lit(I.imm).c_str());
+            else
+                n.data(I);
+        }
+        for (uint32_t r = 0; r < nr; ++r) {
+            if (!wr[r]) continue;
+            if ((int)r == ind) e.line("    L.r%u = n%u;", r, r);
+            else e.line("    L.r%u = a ? n%u : L.r%u;", r, r, r);
+        }
+        if (guarded) {
+            e.line("    L.steps += a ? %uu : 0u;", X.inc);
+            e.line("    a = a & (%s) & (L.steps < lim);", c.c_str());
+        } else {
+            if (ind < 0) e.line("    k += a ? 1u : 0u;");
+            e.line("    a = a & (%s);", c.c_str());
+        }
+        e.line("    }");
+    };
     // guard: steps + g >= budget  <=>  steps >= lim (lim = 0 when budget <= g)
     e.line("    const uint32_t lim = budget > %uu ? budget - %uu : 0u;", G.inc, G.inc);
     e.line("    if (L.steps >= lim) {");
@@ -672,25 +718,33 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("        break;");
     e.line("    }");
     e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
-    e.line("    bool a = true;");
+    e.line("    bool a = true, more = true;");
+    e.line("    {");
+    e.line("    const uint32_t s0 = L.steps;");
+    if (ind >= 0) e.line("    const int64_t i0 = L.r%d;", ind);
+    else e.line("    uint32_t k = 0u;");
+    // after j iterations a lane has steps <= m + j*inc (smax may count lanes
+    // of the group that stopped at the guard above: then T = 0)
+    e.line("    const uint32_t m = smax > s0 ? smax : s0;");
+    e.line("    const uint32_t T = m < lim ? (lim - 1u - m) / %uu : 0u;", X.inc);
+    e.line("    for (uint32_t it = %uu; it <= T; it += %uu) {", kLoopUnroll, kLoopUnroll);
+    for (int u = 0; u < kLoopUnroll; ++u) iteration(false);
+    e.line("    if (!MK_KEEP(a, need)) {");
+    e.line("        more = false;");
+    e.line("        break;");
+    e.line("    }");
+    e.line("    }");
+    if (ind >= 0)
+        e.line("    L.steps = s0 + %uu * (uint32_t)((int64_t)((uint64_t)L.r%d - (uint64_t)i0) / (int64_t)%lld);",
+               X.inc, ind, (long long)step);
+    else
+        e.line("    L.steps = s0 + %uu * k;", X.inc);
+    e.line("    }");
+    e.line("    if (more) {");
     e.line("    do {");
-    for (int u = 0; u < kLoopUnroll; ++u) {
-        e.line("    {");
-        for (uint32_t r = 0; r < rd.size(); ++r)
-            if (rd[r]) e.line("    int64_t n%u = L.r%u;", r, r);
-        OpWriter n{e, w.p, "n"};
-        for (size_t pc = gpc + 1; pc < xpc; ++pc) {
-            const DOp &I = g.D[pc];
-            if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
-            n.data(I);
-        }
-        for (uint32_t r = 0; r < wr.size(); ++r)
-            if (wr[r]) e.line("    L.r%u = a ? n%u : L.r%u;", r, r, r);
-        e.line("    L.steps += a ? %uu : 0u;", X.inc);
-        e.line("    a = a & (%s) & (L.steps < lim);", c.c_str());
-        e.line("    }");
-    }
+    for (int u = 0; u < kLoopUnroll; ++u) iteration(true);
     e.line("    } while (MK_KEEP(a, need));");
+    e.line("    }");
     // a: still in the loop (suspended); otherwise it left through the branch
     // (the condition on its frozen registers fails) or through the guard
     OpWriter l{e, w.p, "L.r"};
@@ -703,14 +757,13 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    L.sb = (a || (%s)) ? (L.steps < lim ? %uu : %uu) : %uu;", cl.c_str(), v, (uint32_t)G.imm, other);
     e.line("    break;");
     e.line("    }");
-    (void)stores;
 }
 
 void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 {
     OpWriter w{e, p, "L.r"};
     const size_t nv = g.entry.size();
-    size_t nloops = 0;
+    std::vector<uint32_t> loops;
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 1");
     e.line("#define MK_SB_DONE 0xFFFFFFFEu");
@@ -734,17 +787,20 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // mk_run(u, ...): superblock variant u for a lane sitting on it (L.sb == u).
     // MK_LOOP_NEED() / MK_KEEP(m, need) come from the includer: the wave's
     // policy for leaving a loop early so that finished lanes can refill.
+    // smax: at least the steps of every lane of the group (self-loops size
+    // their unguarded phase from it; the kernel reduces it over the wave for
+    // loop variants only, see mk_is_loop).
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
-    e.line("                  const uint64_t sstride, const uint32_t pol)");
+    e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
     e.line("{");
-    e.line("    (void)slots; (void)sstride; (void)budget; (void)pol;");
+    e.line("    (void)slots; (void)sstride; (void)budget; (void)pol; (void)smax;");
     e.line("    switch (u) {");
     for (uint32_t v = 0; v < nv; ++v) {
         if (!g.seen[v]) continue;
         e.line("    case %uu: {", v);
         size_t gpc = 0, xpc = 0;
         if (self_loop(g, v, gpc, xpc)) {
-            ++nloops;
+            loops.push_back(v);
             emit_self_loop(w, g, v, gpc, xpc);
             continue;
         }
@@ -810,14 +866,27 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    default: L.sb = MK_SB_DONE; break;");
     e.line("    }");
     e.line("}");
-    e.line("// %zu self-loops", nloops);
+    e.line("// %zu self-loops", loops.size());
+    e.line("MK_FN bool mk_is_loop(const uint32_t u)");
+    e.line("{");
+    if (loops.empty()) {
+        e.line("    (void)u;");
+        e.line("    return false;");
+    } else {
+        e.line("    switch (u) {");
+        for (uint32_t v : loops) e.line("    case %uu:", v);
+        e.line("        return true;");
+        e.line("    default: return false;");
+        e.line("    }");
+    }
+    e.line("}");
     // the whole lane, for the CPU tests (the kernel drives mk_run itself)
     e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
     e.line("{");
     e.line("    MkLane L;");
     e.line("    mk_init(L, in);");
-    e.line("    while (L.sb < MK_SB_DONE) mk_run(L.sb, L, budget, slots, sstride, 0u);");
+    e.line("    while (L.sb < MK_SB_DONE) mk_run(L.sb, L, budget, slots, sstride, 0u, L.steps);");
     e.line("    *steps_out = L.steps;");
     e.line("    *status_out = L.st;");
     e.line("    return L.outv;");
@@ -990,7 +1059,10 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             continue;
         }
         const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
-        if (L.sb == u) mk_run(u, L, p.budget, slots, stride, pol);
+        // loop variants: the group's largest step count (exec is full here,
+        // as the DPP reduction needs; u is uniform)
+        const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
+        if (L.sb == u) mk_run(u, L, p.budget, slots, stride, pol, smax);
     }
     if (p.partials) write_partials(p.partials, gid, cnt);
 }
@@ -1031,6 +1103,9 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("    return c != 0u && c >= need;");
     e.line("}");
     e.line("#define MK_LOOP_NEED(pol) mk_loop_need(pol)");
+    // max over the wave (ockl's DPP reduction: needs the whole wave active), as a scalar
+    e.line("extern \"C\" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);");
+    e.line("#define MK_WAVE_MAX(x) __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32((uint32_t)(x)))");
     e.line("#define MK_KEEP(m, need) mk_keep(m, need)");
     e.s += kDeviceCommon;
     e.s += "\n";
