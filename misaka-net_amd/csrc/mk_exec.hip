@@ -1413,6 +1413,18 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
 }
 
 // ---- tier 3: native kernel per schedule (tis_jit.h) ------------------------
+// Machine-shape policy word (tis_jit.h kJitPolicy); MK_JIT_POLICY="refill,num,min"
+// overrides it for experiments (read when the native kernel is compiled:
+// the word is a constant of the module).
+uint32_t jit_policy()
+{
+    const char *env = std::getenv("MK_JIT_POLICY");
+    unsigned r = 0, nu = 0, mi = 0;
+    if (env && std::sscanf(env, "%u,%u,%u", &r, &nu, &mi) == 3 && r <= 64 && nu <= 16 && mi <= 64)
+        return r | nu << 8 | mi << 16;
+    return kJitPolicy;
+}
+
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
 // gfx950); the code object is loaded per device on first use.  MK_JIT=0 in
 // the environment disables the tier.
@@ -1439,7 +1451,7 @@ bool jit_compile(SchedCache *sc)
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
     J.block = J.heavy ? kJitHeavyBlock : kJitBlock;
-    const std::string src = jit_module_source(lane, J.shape, J.heavy);
+    const std::string src = jit_module_source(lane, J.shape, J.heavy, jit_policy());
     J.src_bytes = src.size();
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
@@ -1483,17 +1495,6 @@ int ensure_jit_device(SchedCache *sc, int d)
         jd.per_cu < 1)
         jd.per_cu = 1;
     return MK_OK;
-}
-
-// Machine-shape policy word (tis_jit.h kJitPolicy); MK_JIT_POLICY="refill,num,min"
-// overrides it for experiments.
-uint32_t jit_policy()
-{
-    const char *env = std::getenv("MK_JIT_POLICY");
-    unsigned r = 0, nu = 0, mi = 0;
-    if (env && std::sscanf(env, "%u,%u,%u", &r, &nu, &mi) == 3 && r <= 64 && nu <= 16 && mi <= 64)
-        return r | nu << 8 | mi << 16;
-    return kJitPolicy;
 }
 
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
@@ -1547,7 +1548,6 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     const uintptr_t va = 4u * kJitStreamLanes;
     p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
                (uintptr_t)d_status % kJitStreamLanes == 0 && (uintptr_t)d_steps % va == 0;
-    p.policy = jit_policy();
     void *args[] = {(void *)&p};
     if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) != hipSuccess)
         return MK_EDEVICE;
@@ -2110,7 +2110,8 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         if (const char *e = std::getenv("MK_JIT_MAX_DOPS")) lim.max_dops = (size_t)std::strtoull(e, nullptr, 10);
         bool heavy = false;
         if (mk::jit_lane_source(sc->prog, lim, lane, why, &shape, nullptr, &heavy))
-            return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM));
+            return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
+                                                                    mk::jit_policy()));
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

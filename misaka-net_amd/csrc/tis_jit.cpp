@@ -643,7 +643,11 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
 // predicated instead of selected) or, without one, a per-lane counter.  Only
 // iterations past T (a launch whose budget ends inside the loop) run the
 // guarded body, which keeps steps exact per iteration.
-constexpr int kLoopUnroll = 4;
+constexpr int kLoopUnroll = 4;      // guarded phase
+constexpr int kLoopUnrollFast = 8;  // unguarded phases, bodies of up to kLoopSmallBody micro-ops
+constexpr size_t kLoopSmallBody = 4;
+
+enum LoopMode { LOOP_GUARDED, LOOP_WIDE, LOOP_NARROW };
 
 void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
 {
@@ -683,32 +687,55 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         if (tk == v && nt != v) c = n.cond(X), other = nt;
         else if (tk != v) c = "!" + n.cond(X), other = tk;
     }
-    // one iteration; guarded: steps counted and the budget checked per iteration
-    auto iteration = [&](bool guarded) {
+    // One iteration.  GUARDED: steps counted and the budget checked per
+    // iteration.  WIDE: no guard, no step counting.  NARROW: as WIDE with the
+    // induction register held in 32 bits (x; exact while it stays in range).
+    auto iteration = [&](LoopMode mode) {
         e.line("    {");
-        for (uint32_t r = 0; r < nr; ++r)
-            if (rd[r]) e.line("    int64_t n%u = L.r%u;", r, r);
+        for (uint32_t r = 0; r < nr; ++r) {
+            if (!rd[r]) continue;
+            if (mode == LOOP_NARROW && (int)r == ind) e.line("    int64_t n%u = (int64_t)x;", r);
+            else e.line("    int64_t n%u = L.r%u;", r, r);
+        }
         OpWriter n{e, w.p, "n"};
         for (size_t pc = gpc + 1; pc < xpc; ++pc) {
             const DOp &I = g.D[pc];
             if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
-            if (I.op == U_ADDI && (int)(I.d / 8) == ind)
-                e.line("    n%d = (int64_t)((uint64_t)n%d + (a ? %s : 0ull));", ind, ind, u64lit(I.imm).c_str());
-            else
+            if (I.op == U_ADDI && (int)(I.d / 8) == ind) {
+                if (mode == LOOP_NARROW) {
+                    e.line("    x = (int32_t)((uint32_t)x + (a ? %uu : 0u));", (uint32_t)(int32_t)I.imm);
+                    e.line("    n%d = (int64_t)x;", ind);
+                } else {
+                    e.line("    n%d = (int64_t)((uint64_t)n%d + (a ? %s : 0ull));", ind, ind, u64lit(I.imm).c_str());
+                }
+            } else {
                 n.data(I);
+            }
         }
         for (uint32_t r = 0; r < nr; ++r) {
             if (!wr[r]) continue;
-            if ((int)r == ind) e.line("    L.r%u = n%u;", r, r);
-            else e.line("    L.r%u = a ? n%u : L.r%u;", r, r, r);
+            if ((int)r == ind) {
+                if (mode != LOOP_NARROW) e.line("    L.r%u = n%u;", r, r);
+            } else {
+                e.line("    L.r%u = a ? n%u : L.r%u;", r, r, r);
+            }
         }
-        if (guarded) {
+        if (mode == LOOP_GUARDED) {
             e.line("    L.steps += a ? %uu : 0u;", X.inc);
             e.line("    a = a & (%s) & (L.steps < lim);", c.c_str());
         } else {
             if (ind < 0) e.line("    k += a ? 1u : 0u;");
             e.line("    a = a & (%s);", c.c_str());
         }
+        e.line("    }");
+    };
+    const int uf = xpc - gpc - 1 <= kLoopSmallBody ? kLoopUnrollFast : kLoopUnroll;
+    // an unguarded phase: chunks of uf iterations while T allows
+    auto phase = [&](LoopMode mode, const char *cap) {
+        e.line("    while (more && %s - it >= %uu) {", cap, uf);
+        e.line("    it += %uu;", uf);
+        for (int u = 0; u < uf; ++u) iteration(mode);
+        e.line("    more = MK_KEEP(a, need);");
         e.line("    }");
     };
     // guard: steps + g >= budget  <=>  steps >= lim (lim = 0 when budget <= g)
@@ -723,17 +750,23 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    const uint32_t s0 = L.steps;");
     if (ind >= 0) e.line("    const int64_t i0 = L.r%d;", ind);
     else e.line("    uint32_t k = 0u;");
-    // after j iterations a lane has steps <= m + j*inc (smax may count lanes
-    // of the group that stopped at the guard above: then T = 0)
-    e.line("    const uint32_t m = smax > s0 ? smax : s0;");
-    e.line("    const uint32_t T = m < lim ? (lim - 1u - m) / %uu : 0u;", X.inc);
-    e.line("    for (uint32_t it = %uu; it <= T; it += %uu) {", kLoopUnroll, kLoopUnroll);
-    for (int u = 0; u < kLoopUnroll; ++u) iteration(false);
-    e.line("    if (!MK_KEEP(a, need)) {");
-    e.line("        more = false;");
-    e.line("        break;");
-    e.line("    }");
-    e.line("    }");
+    // after j iterations a lane has steps <= smax + j*inc (smax is uniform, so
+    // is T; it may count lanes of the group that stopped at the guard above:
+    // then T = 0)
+    e.line("    const uint32_t T = smax < lim ? (lim - 1u - smax) / %uu : 0u;", X.inc);
+    e.line("    uint32_t it = 0u;");
+    if (ind >= 0) {
+        // |x| <= 2^30 at entry and at most (2^30 - 1) / |imm| iterations: x stays in int32
+        const uint64_t ad = step < 0 ? (uint64_t)(-step) : (uint64_t)step;
+        e.line("    if (T >= %uu && MK_ALL(L.r%d >= -0x40000000ll && L.r%d <= 0x40000000ll)) {", uf, ind, ind);
+        e.line("    const uint32_t T32 = T < %lluu ? T : %lluu;", (unsigned long long)(0x3fffffffull / ad),
+               (unsigned long long)(0x3fffffffull / ad));
+        e.line("    int32_t x = (int32_t)L.r%d;", ind);
+        phase(LOOP_NARROW, "T32");
+        e.line("    L.r%d = (int64_t)x;", ind);
+        e.line("    }");
+    }
+    phase(LOOP_WIDE, "T");
     if (ind >= 0)
         e.line("    L.steps = s0 + %uu * (uint32_t)((int64_t)((uint64_t)L.r%d - (uint64_t)i0) / (int64_t)%lld);",
                X.inc, ind, (long long)step);
@@ -742,7 +775,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    }");
     e.line("    if (more) {");
     e.line("    do {");
-    for (int u = 0; u < kLoopUnroll; ++u) iteration(true);
+    for (int u = 0; u < kLoopUnroll; ++u) iteration(LOOP_GUARDED);
     e.line("    } while (MK_KEEP(a, need));");
     e.line("    }");
     // a: still in the loop (suspended); otherwise it left through the branch
@@ -1025,7 +1058,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 {
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     const uint64_t stride = p.lanes;
-    const uint32_t pol = p.policy;
+    const uint32_t pol = MK_POLICY;
     const uint32_t refill_t = pol & 0xffu;
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
@@ -1068,7 +1101,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 }
 )";
 
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy)
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, uint32_t policy)
 {
     Emitter e;
     // hiprtc declares the fixed-width integer types in __hip_internal only
@@ -1090,6 +1123,10 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_ST_STACK_OVERFLOW %d", MK_ST_STACK_OVERFLOW);
     e.line("#define MK_ST_OUTPUT_STOP %d", MK_ST_OUTPUT_STOP);
     e.line("#define MK_FN static __device__ __forceinline__");
+    // machine-shape policy word, a constant of the module so that the loop
+    // exit tests fold (generational: MK_KEEP is "some lane still looping")
+    e.line("#define MK_POLICY 0x%08xu", policy);
+    e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // loop policy of the machine shape (see kMachineKernel)
     e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");
     e.line("{");

@@ -39,7 +39,7 @@ enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
 //   MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *slots,
 //                         uint64_t sstride, uint32_t *steps, uint32_t *status)
 // (the machine shape builds it from mk_init/mk_run, driving MK_LOOP_NEED /
-// MK_KEEP which the includer defines).  `slots` points at stack slot 0 of the
+// MK_KEEP / MK_ALL which the includer defines).  `slots` points at stack slot 0 of the
 // lane, slot s at slots[s * sstride].  MK_FN is defined by the includer.
 // Returns false (why) when over limits.
 // max_steps: the stream shape's longest path in retired instructions (its
@@ -52,7 +52,8 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of
 // the given shape.
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy = false);
+// policy: the machine shape's policy word (kJitPolicy), compiled in.
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, uint32_t policy);
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";

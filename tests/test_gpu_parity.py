@@ -260,7 +260,7 @@ def test_wide_immediates_on_symbolic_acc(gpu, mode):
 # The native tier's two kernel shapes (tis_jit.h): acyclic schedules stream,
 # cyclic ones run as per-lane state machines with refill.  Force the machine
 # shape on every network (MK_JIT_SHAPE is read when a network's kernel is
-# generated) and vary its wave policy (MK_JIT_POLICY, read per launch).
+# generated) and vary its wave policy (MK_JIT_POLICY, compiled into each new network's kernel).
 @pytest.mark.parametrize("policy", ["8,12,16", "1,0,64", "64,16,1", "16,8,4"])
 def test_machine_shape_and_policies(gpu, monkeypatch, policy):
     monkeypatch.setenv("MK_JIT_SHAPE", "machine")

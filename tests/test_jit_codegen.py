@@ -27,6 +27,7 @@ HEADER = """#include <cstdint>
 #define MK_LANE_CHECKED 1
 #define MK_LOOP_NEED(pol) 0u
 #define MK_KEEP(m, need) (m)
+#define MK_ALL(p) (p)
 """
 
 
