@@ -1497,6 +1497,15 @@ int ensure_jit_device(SchedCache *sc, int d)
     return MK_OK;
 }
 
+// Slot memory a heavy-kernel launch may use (tis_jit.h kJitSlotBytes);
+// MK_JIT_SLOT_BYTES overrides it (tests: several launches per batch).
+uint64_t jit_slot_bytes()
+{
+    const char *env = std::getenv("MK_JIT_SLOT_BYTES");
+    const unsigned long long v = env ? std::strtoull(env, nullptr, 10) : 0;
+    return v ? (uint64_t)v : (uint64_t)kJitSlotBytes;
+}
+
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
 int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, uint32_t flags,
@@ -1510,11 +1519,25 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     const SchedProgram &P = sc->prog;
     DeviceGuard g(d);
     const uint64_t block = (uint64_t)sc->jit.block;
-    const uint64_t per_block = sc->jit.shape == JIT_STREAM && !sc->jit.heavy ? block * kJitStreamLanes : block;
-    const uint64_t want = (n + per_block - 1) / per_block;
-    const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
-    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
-    const uint64_t lanes = (uint64_t)blocks * block;
+    const bool heavy = sc->jit.shape == JIT_STREAM && sc->jit.heavy;
+    // heavy: one thread per input, `chunk` inputs per launch (slot memory);
+    // otherwise a resident grid whose threads loop over the inputs
+    uint64_t chunk = n, lanes;
+    int blocks;
+    if (heavy) {
+        if (P.nslots) {
+            const uint64_t fit = jit_slot_bytes() / ((uint64_t)P.nslots * sizeof(int32_t));
+            chunk = std::min<uint64_t>(n, std::max<uint64_t>(block, fit / block * block));
+        }
+        lanes = (std::max<uint64_t>(chunk, 1) + block - 1) / block * block;
+        blocks = (int)(lanes / block);
+    } else {
+        const uint64_t per_block = sc->jit.shape == JIT_STREAM ? block * kJitStreamLanes : block;
+        const uint64_t want = (n + per_block - 1) / per_block;
+        const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
+        blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+        lanes = (uint64_t)blocks * block;
+    }
     if (P.nslots) {
         const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
         if (need > sd.slots_bytes) {
@@ -1540,17 +1563,34 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     p.out = d_out;
     p.status = d_status;
     p.steps = d_steps;
-    if (counting(d_stats, flags) && (rc = ensure_partials(c, lanes))) return rc;
+    // heavy grids may outnumber the partial rows: their waves add atomically
+    if (counting(d_stats, flags) && (rc = ensure_partials(c, heavy ? 0 : lanes))) return rc;
     p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
+    p.part_rows = (uint32_t)(c.partials_bytes / 64);
     p.slots = P.nslots ? sd.d_slots : nullptr;
     p.lanes = lanes;
     p.vlanes = lanes;
     const uintptr_t va = 4u * kJitStreamLanes;
     p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
                (uintptr_t)d_status % kJitStreamLanes == 0 && (uintptr_t)d_steps % va == 0;
-    void *args[] = {(void *)&p};
-    if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) != hipSuccess)
-        return MK_EDEVICE;
+    uint64_t s0 = 0;
+    do {
+        SParams q = p;
+        if (heavy) { // inputs s0 .. s0 + q.n - 1
+            q.n = std::min<uint64_t>(chunk, n - s0);
+            if (in->kind == MK_IN_I64) q.in_data = (const int64_t *)in->data + s0;
+            else if (in->kind == MK_IN_I32) q.in_data = (const int32_t *)in->data + s0;
+            else q.offset = in->offset + s0;
+            q.out = d_out + s0;
+            q.status = d_status + s0;
+            q.steps = d_steps ? d_steps + s0 : nullptr;
+            blocks = (int)std::max<uint64_t>(1, (q.n + block - 1) / block);
+        }
+        void *args[] = {(void *)&q};
+        if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) !=
+            hipSuccess)
+            return MK_EDEVICE;
+    } while (heavy && chunk && (s0 += chunk) < n);
     return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
 

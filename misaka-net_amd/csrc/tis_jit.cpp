@@ -1015,29 +1015,28 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 )";
 
 // Kernel of the stream shape for heavy lanes (more than kJitHeavyOps
-// micro-ops: long programs, deep stacks): one lane per thread, grid-stride,
-// small blocks so that modest batches still spread over every CU, and one
-// copy of the lane code (hiprtc time grows with it).
+// micro-ops: long programs, deep stacks): one lane per thread, small blocks
+// so that modest batches still spread over every CU, and one copy of the
+// lane code (hiprtc time grows with it).  No grid-stride loop: around a
+// lane this long, LLVM hoists the slot addresses of the whole program out
+// of the loop (C4 d1024: 410 VGPRs, one wave per SIMD, vs 50 without the
+// loop); the executor launches one thread per input instead, in chunks
+// bounded by the slot memory they need (kJitSlotBytes).
 static const char *const kStreamKernelHeavy = R"(
-extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
 {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64u + threadIdx.x;
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
-    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
-    uint64_t i = gid;
-    int32_t cur = i < p.n ? sched_input(p, i) : 0;
-    for (; i < p.n; i += stride) {
-        const int32_t nxt = i + stride < p.n ? sched_input(p, i + stride) : 0;
+    if (gid < p.n) {
         uint32_t s, t;
-        const int32_t o = mk_lane_ng(cur, p.budget, slots, p.lanes, &s, &t);
-        p.out[i] = (t & MK_ST_HAS_OUTPUT) ? o : 0;
-        p.status[i] = (uint8_t)t;
-        if (p.steps) p.steps[i] = s;
+        const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, p.slots ? p.slots + gid : (int32_t *)0,
+                                     p.lanes, &s, &t);
+        p.out[gid] = (t & MK_ST_HAS_OUTPUT) ? o : 0;
+        p.status[gid] = (uint8_t)t;
+        if (p.steps) p.steps[gid] = s;
         count_lane(cnt, s, t);
-        cur = nxt;
     }
-    if (p.partials) write_partials(p.partials, gid, cnt);
+    if (p.partials) add_partials(p.partials, p.part_rows, gid, cnt);
 }
 )";
 

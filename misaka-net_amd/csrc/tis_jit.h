@@ -61,6 +61,9 @@ constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
 constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane per thread
 constexpr int kJitHeavyBlock = 64;
+// Heavy kernels run one thread per input; a launch covers at most as many
+// inputs as fit this much stack-slot memory (more take several launches).
+constexpr size_t kJitSlotBytes = size_t(16) << 30;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.

@@ -83,6 +83,30 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode):
     assert (got.status == 0x11).all()
 
 
+# Heavy stream kernels run one thread per input, several launches per batch
+# when the stack slots of the whole batch exceed the slot-memory cap
+# (MK_JIT_SLOT_BYTES=1: 64 inputs per launch); counters included.
+def test_heavy_kernel_chunked_launches(gpu, monkeypatch):
+    import torch
+
+    monkeypatch.setenv("MK_JIT_SLOT_BYTES", "1")
+    nodes = mk.networks.pipeline_network(1024)
+    net = mk.Network(nodes)
+    assert "shape=stream-heavy" in net.plan(), net.plan()
+    n = 1000
+    xs = po.gen_inputs(SEED, n)
+    assert_same(net.compute_batch(xs), oracle(nodes, xs), "c4 D=1024 in 16 launches")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+    net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), stats_ptr=stats.data_ptr(),
+                       gen_kind=N.MK_GEN_FULL, seed=SEED, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = oracle(nodes, po.gen_inputs(SEED, n))
+    assert out.cpu().numpy().tolist() == ref[0].tolist()
+    assert stats[0].item() == int(ref[2].sum()) and stats[2].item() == n
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_c5_zero_trip_and_maximum_trip(gpu, mode):
     nodes = mk.networks.countdown_network()
