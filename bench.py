@@ -39,13 +39,17 @@ K_LANE_OPS = 4  # algorithmic lane-ops per retired node-instruction (BASELINE.md
 HBM_PEAK = 8.0e12
 
 WORKLOADS = {
-    # name: (network factory, lanes per GPU, generator kind, mask, bytes per lane)
+    # name: (workload, network factory, lanes per GPU, generator kind, mask)
     "c2": ("c2_example_net_16M", mk.networks.example_network, 1 << 24, N.MK_GEN_FULL, 0),
     "c3": ("c3_sample_net_8M_per_gpu", mk.networks.sample_network, 1 << 23, N.MK_GEN_FULL, 0),
     "c4": ("c4_pipeline_d64_1M", lambda: mk.networks.pipeline_network(64), 1 << 20, N.MK_GEN_FULL, 0),
     "c4d1024": ("c4_pipeline_d1024_256K", lambda: mk.networks.pipeline_network(1024), 1 << 18, N.MK_GEN_FULL, 0),
     "c5": ("c5_countdown_4M", mk.networks.countdown_network, 1 << 22, N.MK_GEN_MASKED, 1023),
 }
+# Stack-node traffic per lane (PUSH + POP, 4 bytes each), part of the
+# algorithmic bytes: the pipeline's 8 nodes each push `depth` values and pop
+# them all (networks.pipeline_program); the other networks have no stacks.
+STACK_OPS_PER_LANE = {"c4": 2 * 64 * 8, "c4d1024": 2 * 1024 * 8}
 
 
 def log(*a):
@@ -260,7 +264,8 @@ def main():
     # per launch of the executor kernel: algorithmic lane-ops and bytes
     instr_per_launch = retired / world / args.steps
     achieved = K_LANE_OPS * instr_per_launch / launch_max
-    bytes_per_lane = (0 if args.gen_inputs else 4) + 4 + 1  # int32 input read, int32 out + u8 status written
+    # int32 input read, int32 out + u8 status written, stack slots written and read back
+    bytes_per_lane = (0 if args.gen_inputs else 4) + 4 + 1 + 4 * STACK_OPS_PER_LANE.get(args.config, 0)
     bytes_per_launch = bytes_per_lane * lanes
     hbm_achieved = bytes_per_launch / launch_max
     traffic = measured_traffic(name)
