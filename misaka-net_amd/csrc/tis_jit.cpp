@@ -594,6 +594,8 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 0");
     e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_steps);
+    e.line("#define MK_NSLOTS %uu", p.nslots);
+    e.line("#define MK_SLOTS_WAVE_BLOCKED %d", p.nslots <= kJitWaveBlockedSlots ? 1 : 0);
     e.line("#ifdef MK_LANE_CHECKED");
     emit_stream_lane(p, g, e, "mk_lane", false);
     e.line("#endif");
@@ -1029,8 +1031,15 @@ extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
     if (gid < p.n) {
         uint32_t s, t;
+#if MK_SLOTS_WAVE_BLOCKED
+        // the wave's 64 lanes of slot k are 256 contiguous bytes and its slots
+        // follow one another: a wave's stacks are one block (tis_jit.h)
+        int32_t *slots = p.slots ? p.slots + (gid >> 6) * (64ull * MK_NSLOTS) + (gid & 63u) : (int32_t *)0;
+        const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, slots, 64u, &s, &t);
+#else
         const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, p.slots ? p.slots + gid : (int32_t *)0,
                                      p.lanes, &s, &t);
+#endif
         p.out[gid] = (t & MK_ST_HAS_OUTPUT) ? o : 0;
         p.status[gid] = (uint8_t)t;
         if (p.steps) p.steps[gid] = s;

@@ -64,6 +64,12 @@ constexpr int kJitHeavyBlock = 64;
 // Heavy kernels run one thread per input; a launch covers at most as many
 // inputs as fit this much stack-slot memory (more take several launches).
 constexpr size_t kJitSlotBytes = size_t(16) << 30;
+// Heavy-kernel slot layout: up to this many slots per lane, wave-blocked
+// ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, slot
+// offsets are immediates); above it, lane-major ([slot][lanes]).  Measured
+// on MI355X: C4 d64 (328 slots) 593 -> 538 us blocked; C4 d1024 (8,008
+// slots) 3.42 ms lane-major vs 4.14 ms blocked (116 VGPRs instead of 50).
+constexpr uint32_t kJitWaveBlockedSlots = 1024;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.
