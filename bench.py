@@ -43,13 +43,14 @@ WORKLOADS = {
     "c2": ("c2_example_net_16M", mk.networks.example_network, 1 << 24, N.MK_GEN_FULL, 0),
     "c3": ("c3_sample_net_8M_per_gpu", mk.networks.sample_network, 1 << 23, N.MK_GEN_FULL, 0),
     "c4": ("c4_pipeline_d64_1M", lambda: mk.networks.pipeline_network(64), 1 << 20, N.MK_GEN_FULL, 0),
+    "c4d256": ("c4_pipeline_d256_512K", lambda: mk.networks.pipeline_network(256), 1 << 19, N.MK_GEN_FULL, 0),
     "c4d1024": ("c4_pipeline_d1024_256K", lambda: mk.networks.pipeline_network(1024), 1 << 18, N.MK_GEN_FULL, 0),
     "c5": ("c5_countdown_4M", mk.networks.countdown_network, 1 << 22, N.MK_GEN_MASKED, 1023),
 }
 # Stack-node traffic per lane (PUSH + POP, 4 bytes each), part of the
 # algorithmic bytes: the pipeline's 8 nodes each push `depth` values and pop
 # them all (networks.pipeline_program); the other networks have no stacks.
-STACK_OPS_PER_LANE = {"c4": 2 * 64 * 8, "c4d1024": 2 * 1024 * 8}
+STACK_OPS_PER_LANE = {"c4": 2 * 64 * 8, "c4d256": 2 * 256 * 8, "c4d1024": 2 * 1024 * 8}
 
 
 def log(*a):

@@ -682,6 +682,11 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     }
     std::string c = "true";
     uint32_t other = v;
+    // In the unguarded phases a lane that left keeps its registers, so the
+    // exit condition on a register that only changes when the lane is active
+    // (the induction register, or one the body never writes) stays false:
+    // there `a` is the condition itself, one compare and no mask AND.
+    const bool cond_is_flag = X.op == U_BR && ((int)(X.a / 8) == ind || !wr[X.a / 8]);
     if (X.op == U_BR) {
         R(X.a);
         const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
@@ -705,7 +710,10 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
             if (I.op == U_ADDI && (int)(I.d / 8) == ind) {
                 if (mode == LOOP_NARROW) {
-                    e.line("    x = (int32_t)((uint32_t)x + (a ? %uu : 0u));", (uint32_t)(int32_t)I.imm);
+                    if (I.imm == 1 || I.imm == -1) // x -/+ a: one subtract/add with the mask as carry
+                        e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)a);", I.imm < 0 ? '-' : '+');
+                    else
+                        e.line("    x = (int32_t)((uint32_t)x + (a ? %uu : 0u));", (uint32_t)(int32_t)I.imm);
                     e.line("    n%d = (int64_t)x;", ind);
                 } else {
                     e.line("    n%d = (int64_t)((uint64_t)n%d + (a ? %s : 0ull));", ind, ind, u64lit(I.imm).c_str());
@@ -727,7 +735,8 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             e.line("    a = a & (%s) & (L.steps < lim);", c.c_str());
         } else {
             if (ind < 0) e.line("    k += a ? 1u : 0u;");
-            e.line("    a = a & (%s);", c.c_str());
+            if (cond_is_flag) e.line("    a = %s;", c.c_str());
+            else e.line("    a = a & (%s);", c.c_str());
         }
         e.line("    }");
     };

@@ -74,12 +74,13 @@ def test_configs_bit_exact(gpu, name, nodes, n, gen, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_c4_deep_stacks_spill_to_hbm(gpu, mode):
-    nodes = mk.networks.pipeline_network(1024)
+@pytest.mark.parametrize("depth", [256, 1024])
+def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
+    nodes = mk.networks.pipeline_network(depth)
     xs = po.gen_inputs(SEED, 600)
     got = mk.Network(nodes).compute_batch(xs, mode=_m(mode))
     ref = oracle(nodes, xs)
-    assert_same(got, ref, "c4 D=1024")
+    assert_same(got, ref, f"c4 D={depth}")
     assert (got.status == 0x11).all()
 
 
