@@ -23,6 +23,8 @@
 #include <cinttypes>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <vector>
 
@@ -595,7 +597,12 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
     e.line("#define MK_JIT_MACHINE 0");
     e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_steps);
     e.line("#define MK_NSLOTS %uu", p.nslots);
-    e.line("#define MK_SLOTS_WAVE_BLOCKED %d", p.nslots <= kJitWaveBlockedSlots ? 1 : 0);
+    // MK_JIT_SLOT_LAYOUT=blocked|lane overrides the choice (tests, tuning)
+    const char *lay = std::getenv("MK_JIT_SLOT_LAYOUT");
+    const bool blocked = lay && !std::strcmp(lay, "blocked") ? true
+                         : lay && !std::strcmp(lay, "lane") ? false
+                                                             : p.nslots <= kJitWaveBlockedSlots;
+    e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
     e.line("#ifdef MK_LANE_CHECKED");
     emit_stream_lane(p, g, e, "mk_lane", false);
     e.line("#endif");

@@ -67,9 +67,10 @@ constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // Heavy-kernel slot layout: up to this many slots per lane, wave-blocked
 // ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, slot
 // offsets are immediates); above it, lane-major ([slot][lanes]).  Measured
-// on MI355X: C4 d64 (328 slots) 593 -> 538 us blocked; C4 d1024 (8,008
-// slots) 3.42 ms lane-major vs 4.14 ms blocked (116 VGPRs instead of 50).
-constexpr uint32_t kJitWaveBlockedSlots = 1024;
+// on MI355X: C4 d64 (328 slots) 577 -> 539 us blocked; d256 (1,864 slots)
+// 1.51 -> 1.32 ms blocked; d1024 (8,008 slots) 3.42 ms lane-major vs 4.14 ms
+// blocked (116 VGPRs instead of 50).  MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
+constexpr uint32_t kJitWaveBlockedSlots = 4096;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.

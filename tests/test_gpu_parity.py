@@ -84,6 +84,19 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
     assert (got.status == 0x11).all()
 
 
+# Both stack-slot layouts of the heavy kernel (wave-blocked / lane-major),
+# whichever the slot count would pick.
+@pytest.mark.parametrize("layout", ["blocked", "lane"])
+@pytest.mark.parametrize("depth", [64, 1024])
+def test_heavy_kernel_slot_layouts(gpu, monkeypatch, layout, depth):
+    monkeypatch.setenv("MK_JIT_SLOT_LAYOUT", layout)
+    nodes = mk.networks.pipeline_network(depth)
+    net = mk.Network(nodes)
+    assert "shape=stream-heavy" in net.plan(), net.plan()
+    xs = po.gen_inputs(SEED + depth, 1000)
+    assert_same(net.compute_batch(xs), oracle(nodes, xs), f"c4 D={depth} {layout}")
+
+
 # Heavy stream kernels run one thread per input, several launches per batch
 # when the stack slots of the whole batch exceed the slot-memory cap
 # (MK_JIT_SLOT_BYTES=1: 64 inputs per launch); counters included.
