@@ -652,9 +652,11 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
 // predicated instead of selected) or, without one, a per-lane counter.  Only
 // iterations past T (a launch whose budget ends inside the loop) run the
 // guarded body, which keeps steps exact per iteration.
-constexpr int kLoopUnroll = 4;      // guarded phase
-constexpr int kLoopUnrollFast = 8;  // unguarded phases, bodies of up to kLoopSmallBody micro-ops
-constexpr size_t kLoopSmallBody = 4;
+constexpr int kLoopUnroll = 4; // guarded phase
+// Unguarded phases: iterations per exit test, by body size in micro-ops (a
+// test costs ~13 SALU; C5's 1-op bodies on MI355X: 4 -> 578 us, 8 -> 426,
+// 16 -> 401, 32 -> 391).
+int fast_unroll(size_t body_ops) { return body_ops <= 2 ? 32 : body_ops <= 4 ? 16 : body_ops <= 8 ? 8 : 4; }
 
 enum LoopMode { LOOP_GUARDED, LOOP_WIDE, LOOP_NARROW };
 
@@ -747,7 +749,9 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         }
         e.line("    }");
     };
-    const int uf = xpc - gpc - 1 <= kLoopSmallBody ? kLoopUnrollFast : kLoopUnroll;
+    int uf = fast_unroll(xpc - gpc - 1);
+    if (const char *env = std::getenv("MK_JIT_LOOP_UNROLL")) // experiments
+        if (std::atoi(env) >= 1 && std::atoi(env) <= 64) uf = std::atoi(env);
     // an unguarded phase: chunks of uf iterations while T allows
     auto phase = [&](LoopMode mode, const char *cap) {
         e.line("    while (more && %s - it >= %uu) {", cap, uf);
