@@ -10,7 +10,7 @@ import pytest
 import misaka_net_amd as mk
 from misaka_net_amd import _native as N
 from oracle import pyoracle as po
-from tisgen import random_network
+from tisgen import loop_cases, random_network
 
 pytestmark = pytest.mark.gpu
 
@@ -82,6 +82,21 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
     ref = oracle(nodes, xs)
     assert_same(got, ref, f"c4 D={depth}")
     assert (got.status == 0x11).all()
+
+
+# Every path of the machine shape's self-loops (tisgen.loop_cases: 32-bit
+# and 64-bit phases, range checks at +-2^30, step counters, budget-ended
+# loops), once on the default path and once with the machine shape and a
+# policy that leaves loops early (so groups re-enter loops with smaller
+# and mixed step counts).
+@pytest.mark.parametrize("variant", ["auto", "machine-early-exit"])
+def test_loop_phases_bit_exact(gpu, monkeypatch, variant):
+    if variant != "auto":
+        monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+        monkeypatch.setenv("MK_JIT_POLICY", "8,12,16")
+    for label, nodes, xs, kw in loop_cases(n=4096):
+        xs = np.asarray(xs, np.int64)
+        assert_same(mk.Network(nodes).compute_batch(xs, **kw), oracle(nodes, xs, **kw), f"{label} {variant}")
 
 
 # Both stack-slot layouts of the heavy kernel (wave-blocked / lane-major),

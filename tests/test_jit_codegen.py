@@ -16,7 +16,7 @@ import pytest
 import misaka_net_amd as mk
 from oracle import pyoracle as po
 import schedcheck as sc
-from tisgen import random_network
+from tisgen import loop_cases, random_network
 
 SEED = 0x4D49534B41
 
@@ -118,6 +118,12 @@ def test_wide_immediates_and_stop(tmp_path, machine):
              ("budget", loop, [0] * 8, {"budget": 11}),
              ("stop", loop, [0] * 8, {"stop_on_output": True})]
     assert len(check_cases(tmp_path, cases, machine)) == 3
+
+
+def test_loop_phases(tmp_path):
+    # every path of the machine shape's self-loops (tisgen.loop_cases)
+    cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
+    assert len(check_cases(tmp_path, cases, machine=True)) == len(cases)
 
 
 @pytest.mark.parametrize("machine", [False, True])

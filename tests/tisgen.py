@@ -162,3 +162,38 @@ def mutated_program(seed: int) -> str:
     if r.random() < 0.3:
         lines.append("L:")
     return "\n".join(lines)
+
+
+# ---- self-loop shapes of the native machine kernel -----------------------------
+# Each targets one path of the generated loop (tis_jit.cpp emit_self_loop):
+# the 32-bit induction phase and its range check (values near +-2^30, steps
+# of 1 and of ~2^30), the 64-bit phase (int64 wrap), loops with no induction
+# register (step counter), JMP-only loops that only the budget ends, and
+# budgets that end inside a loop (guarded phase).
+def _edge_inputs(rng: random.Random, n: int, lo: int, hi: int) -> list:
+    edges = [0, 1, -1, 2**30, -(2**30), 2**30 + 1, -(2**30) - 1, 2**31 - 1, -(2**31), 2**31 - 2, -(2**31) + 1]
+    return [rng.choice(edges) if rng.random() < 0.2 else rng.randint(lo, hi) for _ in range(n)]
+
+
+def loop_cases(n: int = 512, seed: int = 7):
+    """[(label, nodes, inputs, kwargs)] for the oracle-vs-native loop tests."""
+    rng = random.Random(seed)
+    P = lambda text: [("n", "program", text)]  # noqa: E731
+    return [
+        ("up_by_1", P("IN ACC\nL: ADD 1\nJLZ L\nOUT ACC"), _edge_inputs(rng, n, -3000, 50), {}),
+        ("up_by_1_budget", P("IN ACC\nL: ADD 1\nJLZ L\nOUT ACC"), _edge_inputs(rng, n, -3000, 50),
+         {"budget": 2500}),
+        ("down_by_7", P("IN ACC\nL: SUB 7\nJGZ L\nOUT ACC"), _edge_inputs(rng, n, -50, 20000), {"budget": 5000}),
+        ("down_by_2pow30", P("IN ACC\nL: SUB 1073741823\nJGZ L\nOUT ACC"), _edge_inputs(rng, n, -5, 2**31 - 1), {}),
+        ("swap_loop", P("IN ACC\nSAV\nL: SWP\nADD 1\nSWP\nSUB 1\nJGZ L\nSWP\nOUT ACC"),
+         _edge_inputs(rng, n, -5, 900), {"budget": 6000}),
+        ("jmp_forever", P("IN ACC\nL: ADD 3\nJMP L"), _edge_inputs(rng, n, -100, 100), {"budget": 999}),
+        ("int64_wrap", P("IN ACC\nADD 9223372036854775000\nL: ADD 100\nJGZ L\nOUT ACC"),
+         _edge_inputs(rng, n, -2000, 2000), {}),
+        ("two_loops", [("a", "program", "IN ACC\nL: SUB 1\nJGZ L\nMOV 500, ACC\nM: SUB 2\nJGZ M\nOUT ACC")],
+         _edge_inputs(rng, n, -10, 3000), {}),
+        ("doubling", P("IN ACC\nL: ADD ACC\nJGZ L\nOUT ACC"), _edge_inputs(rng, n, -5, 2**31 - 1), {}),
+        ("neg_sub", P("IN ACC\nL: NEG\nSUB 1\nJLZ L\nOUT ACC"), _edge_inputs(rng, n, -99, 99), {"budget": 777}),
+        ("loop_with_stack", [("a", "program", "IN ACC\nL: PUSH ACC, s\nSUB 1\nJGZ L\nPOP s, ACC\nOUT ACC"),
+                             ("s", "stack", "")], _edge_inputs(rng, n, -3, 40), {"stack_cap": 64}),
+    ]
