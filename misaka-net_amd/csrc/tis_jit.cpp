@@ -362,11 +362,11 @@ struct OpWriter {
         case U_SUB: e.line("    %s%u = (int64_t)((uint64_t)%s - (uint64_t)%s);", R, d, A.c_str(), B.c_str()); return true;
         case U_ADDI: e.line("    %s%u = (int64_t)((uint64_t)%s + %s);", R, d, A.c_str(), u64lit(I.imm).c_str()); return true;
         case U_RSUBI: e.line("    %s%u = (int64_t)(%s - (uint64_t)%s);", R, d, u64lit(I.imm).c_str(), A.c_str()); return true;
-        case U_ST: e.line("    slots[(uint64_t)(%s) * sstride] = (int32_t)%s;", slot, A.c_str()); return true;
+        case U_ST: e.line("    MK_SLOT_ST(slots + (uint64_t)(%s) * sstride, (int32_t)%s);", slot, A.c_str()); return true;
         case U_STI:
-            e.line("    slots[(uint64_t)(%s) * sstride] = (int32_t)%" PRId32 ";", slot, (int32_t)I.imm);
+            e.line("    MK_SLOT_ST(slots + (uint64_t)(%s) * sstride, (int32_t)%" PRId32 ");", slot, (int32_t)I.imm);
             return true;
-        case U_LD: e.line("    %s%u = (int64_t)slots[(uint64_t)(%s) * sstride];", R, d, slot); return true;
+        case U_LD: e.line("    %s%u = (int64_t)MK_SLOT_LD(slots + (uint64_t)(%s) * sstride);", R, d, slot); return true;
         default: return false;
         }
     }
@@ -1155,6 +1155,14 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", policy);
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
+    // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
+    if (const char *nt = std::getenv("MK_JIT_SLOT_NT"); nt && nt[0] == '1') {
+        e.line("#define MK_SLOT_ST(p, v) __builtin_nontemporal_store((v), (p))");
+        e.line("#define MK_SLOT_LD(p) __builtin_nontemporal_load(p)");
+    } else {
+        e.line("#define MK_SLOT_ST(p, v) (*(p) = (v))");
+        e.line("#define MK_SLOT_LD(p) (*(p))");
+    }
     // loop policy of the machine shape (see kMachineKernel)
     e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");
     e.line("{");

@@ -39,8 +39,9 @@ enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
 //   MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *slots,
 //                         uint64_t sstride, uint32_t *steps, uint32_t *status)
 // (the machine shape builds it from mk_init/mk_run, driving MK_LOOP_NEED /
-// MK_KEEP / MK_ALL which the includer defines).  `slots` points at stack slot 0 of the
-// lane, slot s at slots[s * sstride].  MK_FN is defined by the includer.
+// MK_KEEP / MK_ALL; slot accesses go through MK_SLOT_ST / MK_SLOT_LD; the
+// includer defines all five).  `slots` points at stack slot 0 of the lane,
+// slot s at slots[s * sstride].  MK_FN is defined by the includer.
 // Returns false (why) when over limits.
 // max_steps: the stream shape's longest path in retired instructions (its
 // kernel serves launches with a larger budget only); UINT64_MAX for machine.

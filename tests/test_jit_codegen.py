@@ -28,6 +28,8 @@ HEADER = """#include <cstdint>
 #define MK_LOOP_NEED(pol) 0u
 #define MK_KEEP(m, need) (m)
 #define MK_ALL(p) (p)
+#define MK_SLOT_ST(p, v) (*(p) = (v))
+#define MK_SLOT_LD(p) (*(p))
 """
 
 
