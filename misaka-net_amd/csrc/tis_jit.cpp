@@ -660,6 +660,27 @@ int fast_unroll(size_t body_ops) { return body_ops <= 2 ? 32 : body_ops <= 4 ? 1
 
 enum LoopMode { LOOP_GUARDED, LOOP_WIDE, LOOP_NARROW };
 
+// Narrow phase of a loop whose body is only the induction bump x += imm and
+// whose stay condition tests x: the flag can be an int 0/1 from one
+// full-rate VALU op (MK_FLAG_*: x > 0 by med3(x, 0, 1), x < 0 by x >> 31,
+// x != 0 by min_u32(x, 1)) instead of a lane mask.  Returns the macro, or
+// null when the loop does not have that form.
+const char *int_flag_fn(const DOp &X, uint32_t v, int ind, size_t body_ops, int64_t step)
+{
+    if (X.op != U_BR || (int)(X.a / 8) != ind || body_ops != 1) return nullptr;
+    if (!(step == 1 || step == -1 || (step > -(1 << 23) && step < (1 << 23)))) return nullptr;
+    const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
+    if (tk == nt) return nullptr;
+    const bool neg = tk != v; // the loop continues when the condition fails
+    switch ((X.fl >> UF_COND_SHIFT) & 3u) {
+    case 0: return neg ? "MK_FLAG_NZ" : nullptr; // stay while x != 0 (JEZ leaves)
+    case 1: return neg ? nullptr : "MK_FLAG_NZ";
+    case 2: return neg ? nullptr : "MK_FLAG_GT";
+    case 3: return neg ? nullptr : "MK_FLAG_LT";
+    }
+    return nullptr;
+}
+
 void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
 {
     Emitter &e = w.e;
@@ -784,7 +805,25 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         e.line("    const uint32_t T32 = T < %lluu ? T : %lluu;", (unsigned long long)(0x3fffffffull / ad),
                (unsigned long long)(0x3fffffffull / ad));
         e.line("    int32_t x = (int32_t)L.r%d;", ind);
-        phase(LOOP_NARROW, "T32");
+        if (const char *flag = int_flag_fn(X, v, ind, xpc - gpc - 1, step)) {
+            // the whole body is the induction bump: the flag as an int 0/1,
+            // no lane masks (mask-writing VALU ops issue at half rate)
+            e.line("    int32_t f = 1;");
+            e.line("    while (more && T32 - it >= %uu) {", uf);
+            e.line("    it += %uu;", uf);
+            for (int u = 0; u < uf; ++u) {
+                if (step == 1 || step == -1)
+                    e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)f);", step < 0 ? '-' : '+');
+                else
+                    e.line("    x = MK_MAD24(f, %d, x);", (int)step);
+                e.line("    f = %s(x);", flag);
+            }
+            e.line("    more = MK_KEEP(f != 0, need);");
+            e.line("    }");
+            e.line("    a = f != 0;");
+        } else {
+            phase(LOOP_NARROW, "T32");
+        }
         e.line("    L.r%d = (int64_t)x;", ind);
         e.line("    }");
     }
@@ -1155,6 +1194,21 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", policy);
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
+    // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
+    // phase); inline asm so that LLVM does not turn them back into lane masks
+    e.line("MK_FN int32_t mk_flag_gt(int32_t x) { int32_t f; __asm__(\"v_med3_i32 %%0, %%1, 0, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
+    e.line("MK_FN int32_t mk_flag_lt(int32_t x) { int32_t f; __asm__(\"v_lshrrev_b32 %%0, 31, %%1\" : \"=v\"(f) : \"v\"(x)); return f; }");
+    e.line("MK_FN int32_t mk_flag_nz(int32_t x) { int32_t f; __asm__(\"v_min_u32 %%0, %%1, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
+    e.line("MK_FN int32_t mk_mad24(int32_t f, int32_t k, int32_t x)");
+    e.line("{");
+    e.line("    int32_t r;");
+    e.line("    __asm__(\"v_mad_i32_i24 %%0, %%1, %%2, %%3\" : \"=v\"(r) : \"v\"(f), \"v\"(k), \"v\"(x));");
+    e.line("    return r;");
+    e.line("}");
+    e.line("#define MK_FLAG_GT(x) mk_flag_gt(x)");
+    e.line("#define MK_FLAG_LT(x) mk_flag_lt(x)");
+    e.line("#define MK_FLAG_NZ(x) mk_flag_nz(x)");
+    e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (const char *nt = std::getenv("MK_JIT_SLOT_NT"); nt && nt[0] == '1') {
         e.line("#define MK_SLOT_ST(p, v) __builtin_nontemporal_store((v), (p))");

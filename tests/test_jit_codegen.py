@@ -30,6 +30,10 @@ HEADER = """#include <cstdint>
 #define MK_ALL(p) (p)
 #define MK_SLOT_ST(p, v) (*(p) = (v))
 #define MK_SLOT_LD(p) (*(p))
+#define MK_FLAG_GT(x) ((int32_t)((x) > 0))
+#define MK_FLAG_LT(x) ((int32_t)((x) < 0))
+#define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
+#define MK_MAD24(f, k, x) ((int32_t)((uint32_t)(x) + (uint32_t)(f) * (uint32_t)(k)))
 """
 
 

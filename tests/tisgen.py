@@ -192,6 +192,9 @@ def loop_cases(n: int = 512, seed: int = 7):
          _edge_inputs(rng, n, -2000, 2000), {}),
         ("two_loops", [("a", "program", "IN ACC\nL: SUB 1\nJGZ L\nMOV 500, ACC\nM: SUB 2\nJGZ M\nOUT ACC")],
          _edge_inputs(rng, n, -10, 3000), {}),
+        ("down_nz", P("IN ACC\nL: SUB 1\nJNZ L\nOUT ACC"), _edge_inputs(rng, n, -20, 2000), {"budget": 3000}),
+        ("up_to_zero_jez", P("IN ACC\nL: ADD 2\nJEZ E\nJMP L\nE: OUT ACC"), _edge_inputs(rng, n, -2000, 20),
+         {"budget": 3000}),
         ("doubling", P("IN ACC\nL: ADD ACC\nJGZ L\nOUT ACC"), _edge_inputs(rng, n, -5, 2**31 - 1), {}),
         ("neg_sub", P("IN ACC\nL: NEG\nSUB 1\nJLZ L\nOUT ACC"), _edge_inputs(rng, n, -99, 99), {"budget": 777}),
         ("loop_with_stack", [("a", "program", "IN ACC\nL: PUSH ACC, s\nSUB 1\nJGZ L\nPOP s, ACC\nOUT ACC"),

@@ -1,6 +1,9 @@
-// Micro-probe: throughput of the C5 countdown loop shape (x -= flag; flag =
-// x > 0) with 1, 2 or 4 independent chains per thread, 8 waves per SIMD.
-// Tells whether the predicated loop is latency- or issue-bound on gfx950.
+// Micro-probe: throughput of the C5 countdown loop shape on gfx950, full
+// lanes, 8 waves per SIMD.  Variants of one iteration:
+//   mask1/2/4  x -= flag; flag = x > 0   (flag a lane mask: v_subbrev + v_cmp),
+//              1, 2 or 4 independent chains per thread;
+//   int_med3   flag an int 0/1: x -= f; f = med3(x, 0, 1);
+//   int_shift  flag an int 0/1: x -= f; f = (uint)(-x) >> 31.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -27,31 +30,51 @@ __global__ void __launch_bounds__(256) chains(const int *in, int *out, int iters
     out[gid] = s;
 }
 
+template <int V>
+__global__ void __launch_bounds__(256) intflag(const int *in, int *out, int iters)
+{
+    const int gid = blockIdx.x * 256 + threadIdx.x;
+    int x = in[gid] + (1 << 28), f = 1;
+    for (int it = 0; it < iters; it += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            x = (int)((unsigned)x - (unsigned)f);
+            // inline asm keeps LLVM from turning the 0/1 int back into a lane mask
+            if (V == 0) __asm__("v_med3_i32 %0, %1, 0, 1" : "=v"(f) : "v"(x));
+            else __asm__("v_sub_u32 %0, 0, %1\n\tv_lshrrev_b32 %0, 31, %0" : "=&v"(f) : "v"(x));
+        }
+        if (__ballot(f != 0) == 0) break;
+    }
+    out[gid] = x;
+}
+
 int main()
 {
     const int threads = 256 * 256 * 8; // 8 waves per SIMD on 256 CUs
     const int iters = 4096;
     int *in, *out;
-    hipMalloc(&in, sizeof(int) * threads * 4);
-    hipMalloc(&out, sizeof(int) * threads);
-    hipMemset(in, 0, sizeof(int) * threads * 4);
+    (void)hipMalloc(&in, sizeof(int) * threads * 4);
+    (void)hipMalloc(&out, sizeof(int) * threads);
+    (void)hipMemset(in, 0, sizeof(int) * threads * 4);
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    auto run = [&](auto kern, int C) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    auto run = [&](auto kern, int C, const char *name) {
         kern<<<threads / 256, 256>>>(in, out, iters);
-        hipDeviceSynchronize();
-        hipEventRecord(e0);
+        (void)hipDeviceSynchronize();
+        (void)hipEventRecord(e0);
         for (int r = 0; r < 5; ++r) kern<<<threads / 256, 256>>>(in, out, iters);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
         float ms = 0;
-        hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
         const double lane_iters = 5.0 * threads * (double)iters * C;
-        printf("chains=%d  %.3f ms per launch  %.2f T lane-iterations/s\n", C, ms / 5, lane_iters / (ms * 1e-3) / 1e12);
+        printf("%-10s %.3f ms per launch  %.2f T lane-iterations/s\n", name, ms / 5, lane_iters / (ms * 1e-3) / 1e12);
     };
-    run(chains<1>, 1);
-    run(chains<2>, 2);
-    run(chains<4>, 4);
+    run(chains<1>, 1, "mask1");
+    run(chains<2>, 2, "mask2");
+    run(chains<4>, 4, "mask4");
+    run(intflag<0>, 1, "int_med3");
+    run(intflag<1>, 1, "int_shift");
     return 0;
 }
