@@ -299,7 +299,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the host-core baseline is an N=1 figure
             cpu = cpu_baseline(nodes, gen_kind, mask, args.cpu_seconds)
         rec = {
             "metric": METRIC,
