@@ -300,6 +300,36 @@ def test_c3_64m_shard_properties(gpu, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_c5_full_size_properties(gpu, mode):
+    # the C5 bench workload: 4,194,304 lanes, masked inputs 0..1023.  The
+    # network is a function of x alone, so every lane is checked exactly
+    # against an oracle table over all 1024 inputs; out also in closed form:
+    # x <= 0 -> -1, else r = (x - 1) % 3 + 1 selects 112 / 13 / 4 by JRO.
+    n = 1 << 22
+    nodes = mk.networks.countdown_network()
+    out, st, sp, stats = _device_run(mk.Network(nodes), n, gen=(N.MK_GEN_MASKED, 1023), mode=_m(mode))
+    x = po.gen_inputs(SEED, n, kind=N.MK_GEN_MASKED, mask=1023)
+    t_out, t_st, t_sp = oracle(nodes, np.arange(1024, dtype=np.int64))
+    assert np.array_equal(out, t_out[x]) and np.array_equal(st, t_st[x]) and np.array_equal(sp, t_sp[x])
+    r = (x - 1) % 3 + 1
+    assert np.array_equal(out, np.where(x <= 0, -1, np.choose(r - 1, [112, 13, 4])))
+    assert stats[0] == int(sp.astype(np.int64).sum()) and stats[2] == n
+
+
+def test_c4_full_size_properties(gpu):
+    # the C4 d64 bench workload: 1,048,576 lanes; the pipeline's control flow
+    # does not depend on x (every lane retires the same count and outputs);
+    # a seeded slice bit-exact against the oracle
+    n = 1 << 20
+    nodes = mk.networks.pipeline_network(64)
+    out, st, sp, stats = _device_run(mk.Network(nodes), n)
+    sl = slice(n - 2048, n)
+    ref = oracle(nodes, po.gen_inputs(SEED, n)[sl])
+    assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
+    assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_wide_immediates_on_symbolic_acc(gpu, mode):
     # immediates whose low 32-bit word has bit 31 set, applied to a data-dependent ACC
     prog = ("IN ACC\nADD 2147483648\nADD 4294967295\nSUB 2147483649\nADD -4294967296\n"
