@@ -218,9 +218,13 @@ def main():
     e1.record(stream)
     enqueue_s = time.perf_counter() - t0  # host time to issue the timed work
     torch.cuda.synchronize()
+    # This rank's time for its K steps ends when its stream drains; the job's
+    # time is the max over ranks (below). The closing barrier only keeps the
+    # ranks together and is not itself part of any rank's K steps.
+    wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    wall = time.perf_counter() - t0
+        torch.cuda.synchronize()
     kernel_s = e0.elapsed_time(e1) * 1e-3  # HIP events on the launch stream
 
     # Average duration of one executor launch (the dominant kernel) for the
