@@ -362,11 +362,11 @@ struct OpWriter {
         case U_SUB: e.line("    %s%u = (int64_t)((uint64_t)%s - (uint64_t)%s);", R, d, A.c_str(), B.c_str()); return true;
         case U_ADDI: e.line("    %s%u = (int64_t)((uint64_t)%s + %s);", R, d, A.c_str(), u64lit(I.imm).c_str()); return true;
         case U_RSUBI: e.line("    %s%u = (int64_t)(%s - (uint64_t)%s);", R, d, u64lit(I.imm).c_str(), A.c_str()); return true;
-        case U_ST: e.line("    MK_SLOT_ST(slots + (uint64_t)(%s) * sstride, (int32_t)%s);", slot, A.c_str()); return true;
+        case U_ST: e.line("    MK_SLOT_ST(slots, sstride, %s, (int32_t)%s);", slot, A.c_str()); return true;
         case U_STI:
-            e.line("    MK_SLOT_ST(slots + (uint64_t)(%s) * sstride, (int32_t)%" PRId32 ");", slot, (int32_t)I.imm);
+            e.line("    MK_SLOT_ST(slots, sstride, %s, (int32_t)%" PRId32 ");", slot, (int32_t)I.imm);
             return true;
-        case U_LD: e.line("    %s%u = (int64_t)MK_SLOT_LD(slots + (uint64_t)(%s) * sstride);", R, d, slot); return true;
+        case U_LD: e.line("    %s%u = (int64_t)MK_SLOT_LD(slots, sstride, %s);", R, d, slot); return true;
         default: return false;
         }
     }
@@ -603,6 +603,27 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
                          : lay && !std::strcmp(lay, "lane") ? false
                                                              : p.nslots <= kJitWaveBlockedSlots;
     e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
+    if (blocked && g.ndops > kJitHeavyOps) {
+        // Heavy kernel, wave-blocked: `slots` is the wave's block (wave-uniform)
+        // and a slot access is a buffer op whose slot offset s * 256 is a
+        // scalar (SGPR + immediate) and whose lane offset is one VGPR, so no
+        // 64-bit per-lane address is formed or kept live per slot (a deep
+        // pipeline's straight-line pushes otherwise hoist dozens of them).
+        e.line("#ifndef MK_LANE_CHECKED");
+        e.line("#define MK_SLOTS_BUFFER 1");
+        e.line("MK_FN __amdgpu_buffer_rsrc_t mk_slot_rsrc(int32_t *b)");
+        e.line("{");
+        e.line("    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)(256u * MK_NSLOTS), 0x00020000);");
+        e.line("}");
+        e.line("#define MK_SLOT_LANE ((int32_t)((threadIdx.x & 63u) * 4u))");
+        e.line("#undef MK_SLOT_ST");
+        e.line("#undef MK_SLOT_LD");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) \\");
+        e.line("    __builtin_amdgcn_raw_buffer_store_b32((v), mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0)");
+        e.line("#define MK_SLOT_LD(b, ss, s) \\");
+        e.line("    __builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0)");
+        e.line("#endif");
+    }
     e.line("#ifdef MK_LANE_CHECKED");
     emit_stream_lane(p, g, e, "mk_lane", false);
     e.line("#endif");
@@ -1093,7 +1114,12 @@ extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
 #if MK_SLOTS_WAVE_BLOCKED
         // the wave's 64 lanes of slot k are 256 contiguous bytes and its slots
         // follow one another: a wave's stacks are one block (tis_jit.h)
+#if MK_SLOTS_BUFFER
+        // the wave's block; MK_SLOT_ST/LD add the lane's offset
+        int32_t *slots = p.slots ? p.slots + (uint64_t)blockIdx.x * (64ull * MK_NSLOTS) : (int32_t *)0;
+#else
         int32_t *slots = p.slots ? p.slots + (gid >> 6) * (64ull * MK_NSLOTS) + (gid & 63u) : (int32_t *)0;
+#endif
         const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, slots, 64u, &s, &t);
 #else
         const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, p.slots ? p.slots + gid : (int32_t *)0,
@@ -1211,11 +1237,11 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (const char *nt = std::getenv("MK_JIT_SLOT_NT"); nt && nt[0] == '1') {
-        e.line("#define MK_SLOT_ST(p, v) __builtin_nontemporal_store((v), (p))");
-        e.line("#define MK_SLOT_LD(p) __builtin_nontemporal_load(p)");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) __builtin_nontemporal_store((v), (b) + (uint64_t)(s) * (ss))");
+        e.line("#define MK_SLOT_LD(b, ss, s) __builtin_nontemporal_load((b) + (uint64_t)(s) * (ss))");
     } else {
-        e.line("#define MK_SLOT_ST(p, v) (*(p) = (v))");
-        e.line("#define MK_SLOT_LD(p) (*(p))");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))");
+        e.line("#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])");
     }
     // loop policy of the machine shape (see kMachineKernel)
     e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");

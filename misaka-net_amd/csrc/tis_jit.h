@@ -70,7 +70,10 @@ constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // offsets are immediates); above it, lane-major ([slot][lanes]).  Measured
 // on MI355X: C4 d64 (328 slots) 577 -> 539 us blocked; d256 (1,864 slots)
 // 1.51 -> 1.32 ms blocked; d1024 (8,008 slots) 3.42 ms lane-major vs 4.14 ms
-// blocked (116 VGPRs instead of 50).  MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
+// blocked (116 VGPRs instead of 50).  Blocked slots are now buffer ops with a
+// scalar slot offset (emit_stream): d256 1.32 -> 1.23 ms, d1024 blocked 50
+// VGPRs and 3.31 ms = lane-major's 3.29 ms (both HBM-bound on the spill
+// stream).  MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
 constexpr uint32_t kJitWaveBlockedSlots = 4096;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave

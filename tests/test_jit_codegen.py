@@ -28,8 +28,8 @@ HEADER = """#include <cstdint>
 #define MK_LOOP_NEED(pol) 0u
 #define MK_KEEP(m, need) (m)
 #define MK_ALL(p) (p)
-#define MK_SLOT_ST(p, v) (*(p) = (v))
-#define MK_SLOT_LD(p) (*(p))
+#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))
+#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])
 #define MK_FLAG_GT(x) ((int32_t)((x) > 0))
 #define MK_FLAG_LT(x) ((int32_t)((x) < 0))
 #define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
