@@ -380,6 +380,87 @@ struct OpWriter {
     }
 };
 
+// A rolled loop whose body only reads stack slots (a run of POPs: LD ops, no
+// ST) is software-pipelined: while one block of U iterations uses its
+// popped values, the slots of the next block are already being read, so a
+// wave keeps ~kPrefetchLoads spill reads in flight instead of draining its
+// loads at every unrolled step (C4's pop loops are a serial ACC chain over
+// the popped values).  Two register sets (A, B) alternate, so no value is
+// copied while its load is in flight (a copy would need the load's wait).
+// Reading ahead is safe because nothing in the loop writes a slot.  Returns
+// false (nothing emitted) for other runs.
+constexpr size_t kPrefetchLoads = 16;
+
+template <class Expr, class RoundEnd>
+bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::vector<const Run *> &outer,
+                         const Expr &expr, RoundEnd &round_end)
+{
+    if (!r.inner.empty()) return false;
+    if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && env[0] == '0') return false; // experiments
+    std::vector<size_t> lds;
+    for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
+        const DOp &I = g.D[pc];
+        if (I.op == U_ST || I.op == U_STI) return false;
+        if (I.op == U_LD) lds.push_back(pc);
+    }
+    if (lds.empty()) return false;
+    const size_t U = std::max<size_t>(2, kPrefetchLoads / lds.size());
+    if (r.reps < 4 * U) return false;
+    const size_t D = outer.size(), jn = r.reps - r.reps % (2 * U);
+    Emitter &e = w.e;
+    outer.push_back(&r);
+    // set `set` <- block starting at iteration `it`; an index past the loop
+    // is clamped to its last iteration (the final read-ahead re-reads a slot
+    // of the loop instead of leaving its range)
+    auto load = [&](char set, const std::string &it) {
+        for (size_t a = 0; a < lds.size(); ++a)
+            for (size_t k = 0; k < U; ++k)
+                e.line("    { const uint32_t j%zu = %s + %zuu < %zuu ? %s + %zuu : %zuu; "
+                       "%c%zu_%zu_%zu = MK_SLOT_LD(slots, sstride, %s); }",
+                       D, it.c_str(), k, r.reps - 1, it.c_str(), k, r.reps - 1, set, D, a, k,
+                       expr(lds[a], advancing(g.D[lds[a]])).c_str());
+        // keeps the read-ahead here: LLVM otherwise sinks each load to its use
+        e.line("    __asm__ volatile(\"\" ::: \"memory\");");
+    };
+    auto body = [&](char set, const std::string &it) {
+        for (size_t k = 0; k < U; ++k) {
+            e.line("    { const uint32_t j%zu = %s + %zuu; (void)j%zu;", D, it.c_str(), k, D);
+            for (size_t pc = r.start, a = 0; pc < r.start + r.period; ++pc) {
+                const DOp &I = g.D[pc];
+                if (I.op == U_LD) e.line("    %s%u = (int64_t)%c%zu_%zu_%zu;", w.R, I.d / 8, set, D, a++, k);
+                else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+                else w.data(I);
+            }
+            e.line("    }");
+        }
+    };
+    const std::string jb = "jb" + std::to_string(D);
+    e.line("    {");
+    for (char set : {'A', 'B'})
+        for (size_t a = 0; a < lds.size(); ++a)
+            for (size_t k = 0; k < U; ++k) e.line("    int32_t %c%zu_%zu_%zu;", set, D, a, k);
+    load('A', "0u");
+    e.line("    for (uint32_t %s = 0; %s < %zuu; %s += %zuu) {", jb.c_str(), jb.c_str(), jn, jb.c_str(), 2 * U);
+    load('B', jb + " + " + std::to_string(U) + "u");
+    body('A', jb);
+    load('A', jb + " + " + std::to_string(2 * U) + "u");
+    body('B', jb + " + " + std::to_string(U) + "u");
+    e.line("    }");
+    if (jn < r.reps) { // the last reps % 2U iterations, unpipelined
+        e.line("    for (uint32_t j%zu = %zuu; j%zu < %zuu; ++j%zu) {", D, jn, D, r.reps, D);
+        for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
+            const DOp &I = g.D[pc];
+            if (slot_op(I)) w.data(I, expr(pc, advancing(I)).c_str());
+            else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+            else w.data(I);
+        }
+        e.line("    }");
+    }
+    e.line("    }");
+    outer.pop_back();
+    return true;
+}
+
 // Emits the body [lo, hi) of a variant -- data ops and ROUND_END markers --
 // rolling `runs` into nested for loops (loop variables j0, j1, ...); an
 // op's slot or step count is its value in the first copy plus, per
@@ -401,6 +482,10 @@ void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs
     for (size_t pc = lo; pc < hi;) {
         if (ri < runs.size() && runs[ri].start == pc) {
             const Run &r = runs[ri++];
+            if (emit_prefetched_run(w, g, r, outer, expr, round_end)) {
+                pc += r.reps * r.period;
+                continue;
+            }
             w.e.line("    for (uint32_t j%zu = 0; j%zu < %zuu; ++j%zu) {", outer.size(), outer.size(), r.reps,
                      outer.size());
             outer.push_back(&r);
@@ -591,6 +676,14 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
 // (MK_MAX_STEPS): its lane function has no guards and no checked variants.
 // The guarded lane (MK_LANE_CHECKED) is for the CPU tests; the executor
 // gives launches with a smaller budget to tier 2.
+// Stream lanes with more micro-ops than this run in the heavy kernel
+// (kJitHeavyOps; MK_JIT_HEAVY_OPS overrides it for tests and tuning).
+size_t jit_heavy_ops()
+{
+    const char *env = std::getenv("MK_JIT_HEAVY_OPS");
+    return env && *env ? (size_t)std::strtoull(env, nullptr, 10) : kJitHeavyOps;
+}
+
 void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps)
 {
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
@@ -603,7 +696,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
                          : lay && !std::strcmp(lay, "lane") ? false
                                                              : p.nslots <= kJitWaveBlockedSlots;
     e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
-    if (blocked && g.ndops > kJitHeavyOps) {
+    if (blocked && g.ndops > jit_heavy_ops()) {
         // Heavy kernel, wave-blocked: `slots` is the wave's block (wave-uniform)
         // and a slot access is a buffer op whose slot offset s * 256 is a
         // scalar (SGPR + immediate) and whose lane offset is one VGPR, so no
@@ -621,7 +714,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOT_ST(b, ss, s, v) \\");
         e.line("    __builtin_amdgcn_raw_buffer_store_b32((v), mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0)");
         e.line("#define MK_SLOT_LD(b, ss, s) \\");
-        e.line("    __builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0)");
+        e.line("    ((int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0))");
         e.line("#endif");
     }
     e.line("#ifdef MK_LANE_CHECKED");
@@ -1023,7 +1116,7 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
         emit_stream(p, g, e, max_fast_steps(p, g));
     if (shape) *shape = s;
     if (max_steps) *max_steps = s == JIT_STREAM ? max_fast_steps(p, g) : UINT64_MAX;
-    if (heavy) *heavy = g.ndops > kJitHeavyOps;
+    if (heavy) *heavy = g.ndops > jit_heavy_ops();
     src = std::move(e.s);
     return true;
 }

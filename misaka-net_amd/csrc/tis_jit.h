@@ -66,15 +66,15 @@ constexpr int kJitHeavyBlock = 64;
 // inputs as fit this much stack-slot memory (more take several launches).
 constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // Heavy-kernel slot layout: up to this many slots per lane, wave-blocked
-// ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, slot
-// offsets are immediates); above it, lane-major ([slot][lanes]).  Measured
-// on MI355X: C4 d64 (328 slots) 577 -> 539 us blocked; d256 (1,864 slots)
-// 1.51 -> 1.32 ms blocked; d1024 (8,008 slots) 3.42 ms lane-major vs 4.14 ms
-// blocked (116 VGPRs instead of 50).  Blocked slots are now buffer ops with a
-// scalar slot offset (emit_stream): d256 1.32 -> 1.23 ms, d1024 blocked 50
-// VGPRs and 3.31 ms = lane-major's 3.29 ms (both HBM-bound on the spill
-// stream).  MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
-constexpr uint32_t kJitWaveBlockedSlots = 4096;
+// ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, read
+// and written by buffer ops whose slot offset s * 256 is a scalar, which
+// bounds the block to 2^31 bytes); above it, lane-major ([slot][lanes]).
+// Measured on MI355X: C4 d64 (328 slots) 577 -> 539 us blocked; d256 (1,864
+// slots) 1.51 -> 1.32 ms blocked, 1.23 ms with buffer ops; d1024 (8,008
+// slots) with pipelined pops 2.97 ms blocked vs 3.18 ms lane-major (before
+// the buffer ops, blocked held 116 VGPRs and lost: 4.14 vs 3.42 ms).
+// MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
+constexpr uint32_t kJitWaveBlockedSlots = 1u << 22;
 
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.

@@ -80,8 +80,14 @@ def pipeline_program(k: int, nodes: int, depth: int) -> str:
             f"QL: POP {stk}, ACC",
             f"MOV ACC, {me}:R2",
             "SWP",
-            "ADD ACC",  # sum = 4*sum + v: order dependent, so LIFO order is checked
+            # sum = 3*sum + v: order dependent, so LIFO order is checked, and
+            # with an odd multiplier (invertible mod 2^32) every popped value
+            # reaches the int32 output.  (4*sum + v, used before, left only
+            # the last 16 pops live in the low 32 bits, and a compiler may
+            # drop the others' loads.)
+            f"MOV ACC, {me}:R3",
             "ADD ACC",
+            "ADD R3",
             "ADD R2",
             "SAV",
             "MOV R1, ACC",

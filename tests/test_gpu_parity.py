@@ -112,6 +112,35 @@ def test_heavy_kernel_slot_layouts(gpu, monkeypatch, layout, depth):
     assert_same(net.compute_batch(xs), oracle(nodes, xs), f"c4 D={depth} {layout}")
 
 
+def signed_pop_network(depth):
+    """Pushes x - 7i (int32), pops them into an int64 sum and branches on its
+    sign: a popped value that were zero-extended instead of sign-extended
+    (stack.go:113 -> program.go:163 round trip) would flip the branch."""
+    prog = "\n".join(
+        ["IN ACC", "SAV", f"MOV {depth}, ACC", "PL: SWP", "SUB 7", "PUSH ACC, s0", "SWP", "SUB 1", "JGZ PL",
+         "MOV 0, ACC", "SAV", f"MOV {depth}, ACC", "MOV ACC, p0:R1", "QL: POP s0, ACC", "MOV ACC, p0:R2", "SWP",
+         "ADD R2", "SAV", "MOV R1, ACC", "SUB 1", "MOV ACC, p0:R1", "JGZ QL", "SWP", "JLZ NEG", "OUT 1", "JMP E",
+         "NEG: OUT -1", "E: NOP", ""]
+    )
+    return [mk.networks.NodeSpec("p0", "program", prog), mk.networks.NodeSpec("s0", "stack")]
+
+
+# Popped values are sign-extended in every slot layout of the heavy kernel
+# (the wave-blocked one reads slots with unsigned 32-bit buffer loads).
+@pytest.mark.parametrize("layout", ["blocked", "lane"])
+@pytest.mark.parametrize("depth", [64, 300])
+def test_heavy_kernel_pops_sign_extend(gpu, monkeypatch, layout, depth):
+    monkeypatch.setenv("MK_JIT_SLOT_LAYOUT", layout)
+    monkeypatch.setenv("MK_JIT_HEAVY_OPS", "16")
+    nodes = signed_pop_network(depth)
+    net = mk.Network(nodes)
+    assert "shape=stream-heavy" in net.plan(), net.plan()
+    xs = po.gen_inputs(SEED + 7 * depth, 1000)
+    ref = oracle(nodes, xs)
+    assert {1, -1} <= set(ref[0].tolist())
+    assert_same(net.compute_batch(xs), ref, f"signed pops D={depth} {layout}")
+
+
 # Heavy stream kernels run one thread per input, several launches per batch
 # when the stack slots of the whole batch exceed the slot-memory cap
 # (MK_JIT_SLOT_BYTES=1: 64 inputs per launch); counters included.
