@@ -396,7 +396,9 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
                          const Expr &expr, RoundEnd &round_end)
 {
     if (!r.inner.empty()) return false;
-    if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && env[0] == '0') return false; // experiments
+    size_t depth = kPrefetchLoads; // MK_JIT_PREFETCH=<loads in flight>, 0 = off (experiments)
+    if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && *env) depth = (size_t)std::strtoull(env, nullptr, 10);
+    if (!depth) return false;
     std::vector<size_t> lds;
     for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
         const DOp &I = g.D[pc];
@@ -404,7 +406,7 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
         if (I.op == U_LD) lds.push_back(pc);
     }
     if (lds.empty()) return false;
-    const size_t U = std::max<size_t>(2, kPrefetchLoads / lds.size());
+    const size_t U = std::max<size_t>(2, depth / lds.size());
     if (r.reps < 4 * U) return false;
     const size_t D = outer.size(), jn = r.reps - r.reps % (2 * U);
     Emitter &e = w.e;
