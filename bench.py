@@ -129,6 +129,9 @@ def main():
                     help="every rank on cuda:0 (rehearse the multi-rank path on one GPU, with --dist-backend gloo)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--host-io", action="store_true",
+                    help="also time mk_compute_batch on host buffers (int64 in, int32 out + u8 status over PCIe); "
+                         "reported as host_io, never as value")
     args = ap.parse_args()
     if args.interp:
         args.mode = "interp"
@@ -257,6 +260,25 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
+    host_io = None
+    if args.host_io and rank == 0:
+        # the host-buffer boundary (mk_compute_batch): inputs as int64 /compute
+        # values in pageable host memory, outputs and statuses copied back
+        xh = x.cpu().numpy().astype(np.int64)
+        net.compute_batch(xh, steps=False, mode=args.mode)  # warm (allocations)
+        reps = max(1, min(args.steps, 5))
+        th = time.perf_counter()
+        for _ in range(reps):
+            net.compute_batch(xh, steps=False, mode=args.mode)
+        dt = (time.perf_counter() - th) / reps
+        host_io = {
+            "ms_per_call": dt * 1e3,
+            "node_instr_per_s": retired / (world * args.steps) / dt,
+            "results_per_s": with_out / (world * args.steps) / dt,
+            "bytes_per_lane": 8 + 4 + 1,
+            "note": "pageable host buffers, PCIe-inclusive; not the value",
+        }
+
     value = retired / wall_max
     per_gpu_kernel_rate = retired / world / kern_max
     peak_meas = None
@@ -338,6 +360,8 @@ def main():
         }
         if gather_ms is not None:
             rec["gather_ms"] = gather_ms
+        if host_io is not None:
+            rec["host_io"] = host_io
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
