@@ -48,6 +48,28 @@ __global__ void __launch_bounds__(256) intflag(const int *in, int *out, int iter
     out[gid] = x;
 }
 
+// int_fused: the bump and the flag in one asm block (no compiler s_nop
+// between them); int_med3x2: two independent int-flag chains per thread.
+template <int C>
+__global__ void __launch_bounds__(256) intfused(const int *in, int *out, int iters)
+{
+    const int gid = blockIdx.x * 256 + threadIdx.x;
+    int x[C], f[C];
+    for (int c = 0; c < C; ++c) x[c] = in[gid * C + c] + (1 << 28), f[c] = 1;
+    for (int it = 0; it < iters; it += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                __asm__("v_sub_u32 %0, %0, %1\n\tv_med3_i32 %1, %0, 0, 1" : "+v"(x[c]), "+v"(f[c]));
+        }
+        if (__ballot(f[0] != 0) == 0) break;
+    }
+    int s = 0;
+    for (int c = 0; c < C; ++c) s += x[c];
+    out[gid] = s;
+}
+
 int main()
 {
     const int threads = 256 * 256 * 8; // 8 waves per SIMD on 256 CUs
@@ -76,5 +98,8 @@ int main()
     run(chains<4>, 4, "mask4");
     run(intflag<0>, 1, "int_med3");
     run(intflag<1>, 1, "int_shift");
+    run(intfused<1>, 1, "int_fused");
+    run(intfused<2>, 2, "int_fusedx2");
+    run(intfused<4>, 4, "int_fusedx4");
     return 0;
 }
