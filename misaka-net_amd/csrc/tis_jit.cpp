@@ -395,7 +395,10 @@ template <class Expr, class RoundEnd>
 bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::vector<const Run *> &outer,
                          const Expr &expr, RoundEnd &round_end)
 {
-    if (!r.inner.empty()) return false;
+    // stream shapes only: the machine shape's lane registers live in a struct
+    // (L.r*) and a pipelined pop loop there compiled in seconds alone but
+    // stalled hiprtc for minutes inside the GPU test process (r01u)
+    if (!r.inner.empty() || std::strcmp(w.R, "r") != 0) return false;
     size_t depth = kPrefetchLoads; // MK_JIT_PREFETCH=<loads in flight>, 0 = off (experiments)
     if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && *env) depth = (size_t)std::strtoull(env, nullptr, 10);
     if (!depth) return false;

@@ -141,6 +141,26 @@ def test_heavy_kernel_pops_sign_extend(gpu, monkeypatch, layout, depth):
     assert_same(net.compute_batch(xs), ref, f"signed pops D={depth} {layout}")
 
 
+# Pipelined POP loops (emit_prefetched_run: reps >= 64) in both stream
+# kernels: the light one (4 lanes per thread, lane-major slots) and the heavy
+# one (wave-blocked buffer slots); the machine shape keeps plain loops.
+@pytest.mark.parametrize("shape", ["light", "heavy", "machine"])
+def test_pipelined_pops_every_shape(gpu, monkeypatch, shape):
+    if shape == "heavy":
+        monkeypatch.setenv("MK_JIT_HEAVY_OPS", "16")
+    if shape == "machine":
+        monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+    for nodes in (signed_pop_network(300), mk.networks.pipeline_network(256)):
+        net = mk.Network(nodes)
+        plan = net.plan()
+        want = {"light": "shape=stream ", "heavy": "shape=stream-heavy", "machine": "shape=machine"}[shape]
+        if shape == "light" and "shape=stream-heavy" in plan:
+            continue  # the 8-node pipeline is heavy by size
+        assert want in plan + " ", plan
+        xs = po.gen_inputs(SEED + 3, 777)
+        assert_same(net.compute_batch(xs), oracle(nodes, xs), f"pipelined pops {shape}")
+
+
 # Heavy stream kernels run one thread per input, several launches per batch
 # when the stack slots of the whole batch exceed the slot-memory cap
 # (MK_JIT_SLOT_BYTES=1: 64 inputs per launch); counters included.
