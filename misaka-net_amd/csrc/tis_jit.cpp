@@ -395,9 +395,8 @@ template <class Expr, class RoundEnd>
 bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::vector<const Run *> &outer,
                          const Expr &expr, RoundEnd &round_end)
 {
-    // stream shapes only: the machine shape's lane registers live in a struct
-    // (L.r*) and a pipelined pop loop there compiled in seconds alone but
-    // stalled hiprtc for minutes inside the GPU test process (r01u)
+    // stream shapes only (the machine shape, whose lane registers live in a
+    // struct, L.r*, was checked bit-exact with it but not measured)
     if (!r.inner.empty() || std::strcmp(w.R, "r") != 0) return false;
     size_t depth = kPrefetchLoads; // MK_JIT_PREFETCH=<loads in flight>, 0 = off (experiments)
     if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && *env) depth = (size_t)std::strtoull(env, nullptr, 10);
