@@ -319,6 +319,12 @@ def main():
         "peak_measured": None if peak_meas is None else peak_meas / 1e12,
         "launch_us": launch_max * 1e6,
     }
+    if hbm["frac"] > 1.0:
+        hbm["note"] = ("algorithmic bytes above the HBM peak: stack slots written and popped back while still in "
+                       "L2/MALL; `traffic` (PMC) is what reached HBM")
+    if issue["frac"] > 1.0:
+        issue["note"] = ("k = 4 lane-ops per node-instruction is the frozen model; the schedule compiler turns "
+                         "port hand-offs, SWP/SAV and loop control into register renames, so fewer are issued")
     # The dominant kernel's roofline is the tighter of the two bounds: the
     # byte stream for short networks (C2, C3), integer issue for long ones.
     hbm_bound = hbm_achieved / HBM_PEAK >= achieved / peak
