@@ -1168,9 +1168,9 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
         o2 = (t2 & MK_ST_HAS_OUTPUT) ? o2 : 0;
         o3 = (t3 & MK_ST_HAS_OUTPUT) ? o3 : 0;
         if (p.io_vec && base + 4 <= p.n) {
-            *reinterpret_cast<int4 *>(p.out + base) = make_int4(o0, o1, o2, o3);
-            *reinterpret_cast<uint32_t *>(p.status + base) =
-                (t0 & 0xffu) | (t1 & 0xffu) << 8 | (t2 & 0xffu) << 16 | t3 << 24;
+            MK_IO_ST(reinterpret_cast<mk_i32x4 *>(p.out + base), (mk_i32x4{o0, o1, o2, o3}));
+            MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base),
+                     (t0 & 0xffu) | (t1 & 0xffu) << 8 | (t2 & 0xffu) << 16 | t3 << 24);
             if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base) = make_uint4(s0, s1, s2, s3);
             count_lane(cnt, s0, t0);
             count_lane(cnt, s1, t1);
@@ -1340,6 +1340,12 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
         e.line("#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))");
         e.line("#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])");
     }
+    // vector out/status stores of the light stream kernel (MK_JIT_IO_NT=1: non-temporal, experiments)
+    e.line("typedef int32_t mk_i32x4 __attribute__((ext_vector_type(4)));");
+    if (const char *nt = std::getenv("MK_JIT_IO_NT"); nt && nt[0] == '1')
+        e.line("#define MK_IO_ST(ptr, v) __builtin_nontemporal_store((v), (ptr))");
+    else
+        e.line("#define MK_IO_ST(ptr, v) (*(ptr) = (v))");
     // loop policy of the machine shape (see kMachineKernel)
     e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");
     e.line("{");

@@ -151,9 +151,13 @@ def test_shapes():
     assert shape == "machine" and "do {" in src
 
 
-def test_module_compiles_for_gfx950():
+@pytest.mark.parametrize("which,io_nt", [("countdown", "0"), ("example", "0"), ("example", "1")])
+def test_module_compiles_for_gfx950(which, io_nt, monkeypatch):
     # hiprtc in-process, no GPU: the product library reports the native tier
-    net = mk.Network(mk.networks.countdown_network())
+    # for both shapes (machine: countdown; light stream: example), and with
+    # the non-temporal out/status stores (MK_JIT_IO_NT=1)
+    monkeypatch.setenv("MK_JIT_IO_NT", io_nt)
+    net = mk.Network(getattr(mk.networks, f"{which}_network")())
     plan = net.plan(mode="jit")
     assert plan.startswith("tier=native "), plan
     src = net.jit_source()
