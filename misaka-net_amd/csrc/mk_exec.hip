@@ -28,12 +28,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mk.h"
@@ -1124,6 +1126,7 @@ struct mk_net {
     std::mutex mu;      // serialises host-API calls, compilation and device-context setup
     mk::DevCtx dev[mk::kMaxDevices];
     std::vector<std::unique_ptr<mk::SchedCache>> sched;
+    mk::JitLimits jit_lim = mk::JitLimits::from_env(); // knob snapshot at load (tis_jit.h)
     ~mk_net()
     {
         int prev = 0;
@@ -1413,22 +1416,60 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
 }
 
 // ---- tier 3: native kernel per schedule (tis_jit.h) ------------------------
-// Machine-shape policy word (tis_jit.h kJitPolicy); MK_JIT_POLICY="refill,num,min"
-// overrides it for experiments (read when the native kernel is compiled:
-// the word is a constant of the module).
-uint32_t jit_policy()
+// One hiprtc compilation, run on a helper thread so that the caller can give
+// up after lim.max_compile_s: the job owns its inputs and outputs (shared),
+// so a compile the caller abandoned finishes in the background and is
+// discarded.
+struct HiprtcJob {
+    std::string src;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, ok = false;
+    std::string why;
+    std::vector<char> code;
+};
+
+void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
 {
-    const char *env = std::getenv("MK_JIT_POLICY");
-    unsigned r = 0, nu = 0, mi = 0;
-    if (env && std::sscanf(env, "%u,%u,%u", &r, &nu, &mi) == 3 && r <= 64 && nu <= 16 && mi <= 64)
-        return r | nu << 8 | mi << 16;
-    return kJitPolicy;
+    bool ok = false;
+    std::string why;
+    std::vector<char> code;
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        why = "hiprtcCreateProgram failed";
+    } else {
+        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+        const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+        size_t cs = 0;
+        if (r != HIPRTC_SUCCESS) {
+            size_t ls = 0;
+            (void)hiprtcGetProgramLogSize(prog, &ls);
+            std::string log(ls, '\0');
+            if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
+            why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
+        } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+            why = "hiprtc produced no code";
+        } else {
+            code.resize(cs);
+            (void)hiprtcGetCode(prog, code.data());
+            ok = true;
+        }
+        (void)hiprtcDestroyProgram(&prog);
+    }
+    std::lock_guard<std::mutex> lk(j->mu);
+    j->ok = ok;
+    j->why = std::move(why);
+    j->code = std::move(code);
+    j->done = true;
+    j->cv.notify_all();
 }
 
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
-// gfx950); the code object is loaded per device on first use.  MK_JIT=0 in
-// the environment disables the tier.
-bool jit_compile(SchedCache *sc)
+// gfx950); the code object is loaded per device on first use.  Bounded:
+// a lane source over lim.max_src_bytes is not compiled, and a compile that
+// takes longer than lim.max_compile_s is abandoned -- either way the
+// network stays on tier 2 with the reason in mk_net_plan.
+bool jit_compile(SchedCache *sc, const JitLimits &lim)
 {
     JitState &J = sc->jit;
     if (J.tried) return J.ok;
@@ -1437,47 +1478,40 @@ bool jit_compile(SchedCache *sc)
         J.why = "no compiled schedule (" + sc->why + ")";
         return false;
     }
-    const char *env = std::getenv("MK_JIT");
-    if (env && std::strcmp(env, "0") == 0) {
+    if (lim.disabled) {
         J.why = "disabled by MK_JIT=0";
         return false;
     }
     const auto t0 = std::chrono::steady_clock::now();
     std::string lane;
-    JitLimits lim;
-    const char *shp = std::getenv("MK_JIT_SHAPE"); // "machine" / "stream": force a shape (experiments)
-    lim.force_machine = shp && std::strcmp(shp, "machine") == 0;
-    lim.force_stream = shp && std::strcmp(shp, "stream") == 0;
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
     J.block = J.heavy ? kJitHeavyBlock : kJitBlock;
-    const std::string src = jit_module_source(lane, J.shape, J.heavy, jit_policy());
-    J.src_bytes = src.size();
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-        J.why = "hiprtcCreateProgram failed";
+    if (lane.size() > lim.max_src_bytes) {
+        J.why = "lane source of " + std::to_string(lane.size()) + " B exceeds the native tier's compile bound (" +
+                std::to_string(lim.max_src_bytes) + " B)";
         return false;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
-    if (r != HIPRTC_SUCCESS) {
-        size_t ls = 0;
-        (void)hiprtcGetProgramLogSize(prog, &ls);
-        std::string log(ls, '\0');
-        if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
-        J.why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
-        (void)hiprtcDestroyProgram(&prog);
-        return false;
+    auto job = std::make_shared<HiprtcJob>();
+    job->src = jit_module_source(lane, J.shape, J.heavy, lim);
+    J.src_bytes = job->src.size();
+    std::thread(hiprtc_run, job).detach();
+    {
+        std::unique_lock<std::mutex> lk(job->mu);
+        const auto limit = std::chrono::duration<double>(lim.max_compile_s);
+        if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+            char b[128];
+            snprintf(b, sizeof b, "hiprtc did not finish within the native tier's compile bound (%.0f s)",
+                     lim.max_compile_s);
+            J.why = b;
+            return false;
+        }
+        if (!job->ok) {
+            J.why = job->why;
+            return false;
+        }
+        J.code = std::move(job->code);
     }
-    size_t cs = 0;
-    if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
-        J.why = "hiprtc produced no code";
-        (void)hiprtcDestroyProgram(&prog);
-        return false;
-    }
-    J.code.resize(cs);
-    (void)hiprtcGetCode(prog, J.code.data());
-    (void)hiprtcDestroyProgram(&prog);
     J.compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     J.ok = true;
     return true;
@@ -1495,15 +1529,6 @@ int ensure_jit_device(SchedCache *sc, int d)
         jd.per_cu < 1)
         jd.per_cu = 1;
     return MK_OK;
-}
-
-// Slot memory a heavy-kernel launch may use (tis_jit.h kJitSlotBytes);
-// MK_JIT_SLOT_BYTES overrides it (tests: several launches per batch).
-uint64_t jit_slot_bytes()
-{
-    const char *env = std::getenv("MK_JIT_SLOT_BYTES");
-    const unsigned long long v = env ? std::strtoull(env, nullptr, 10) : 0;
-    return v ? (uint64_t)v : (uint64_t)kJitSlotBytes;
 }
 
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
@@ -1526,7 +1551,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     int blocks;
     if (heavy) {
         if (P.nslots) {
-            const uint64_t fit = jit_slot_bytes() / ((uint64_t)P.nslots * sizeof(int32_t));
+            const uint64_t fit = h->jit_lim.slot_bytes / ((uint64_t)P.nslots * sizeof(int32_t));
             chunk = std::min<uint64_t>(n, std::max<uint64_t>(block, fit / block * block));
         }
         lanes = (std::max<uint64_t>(chunk, 1) + block - 1) / block * block;
@@ -1608,7 +1633,7 @@ Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, uint32_t budget, SchedCa
     SchedCache *sc = get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
     *out = sc;
     const bool want_jit = (flags & MK_FLAG_JIT) || !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL));
-    if (want_jit && jit_compile(sc) && (sc->jit.shape == JIT_MACHINE || (uint64_t)budget > sc->jit.max_steps))
+    if (want_jit && jit_compile(sc, h->jit_lim) && (sc->jit.shape == JIT_MACHINE || (uint64_t)budget > sc->jit.max_steps))
         return TIER_NATIVE;
     if (flags & MK_FLAG_JIT) return TIER_NONE;
     return sc->ok ? TIER_COMPILED : TIER_INTERP;
@@ -2104,7 +2129,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                  sc->jit.shape == mk::JIT_MACHINE ? "machine" : sc->jit.heavy ? "stream-heavy" : "stream",
                  sc->jit.src_bytes, sc->jit.code.size(),
                  sc->jit.compile_s);
-        s = std::string("tier=native ") + buf + tail;
+        s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
     } else {
         const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
         uint32_t B, K;
@@ -2146,12 +2171,10 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (!sc->ok) why = sc->why;
     else {
         mk::JitShape shape;
-        mk::JitLimits lim;
-        if (const char *e = std::getenv("MK_JIT_MAX_DOPS")) lim.max_dops = (size_t)std::strtoull(e, nullptr, 10);
         bool heavy = false;
-        if (mk::jit_lane_source(sc->prog, lim, lane, why, &shape, nullptr, &heavy))
+        if (mk::jit_lane_source(sc->prog, h->jit_lim, lane, why, &shape, nullptr, &heavy))
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
-                                                                    mk::jit_policy()));
+                                                                    h->jit_lim));
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

@@ -155,11 +155,12 @@ int mkc_jit_lane(void *hv, uint32_t cap, int soo, int force_machine, uint32_t *n
     mk::SchedProgram P;
     std::string w, src;
     mk::SchedLimits lim;
-    mk::JitLimits jl;
+    mk::JitLimits jl = mk::JitLimits::from_env();
     jl.force_machine = force_machine != 0;
+    if (force_machine) jl.force_stream = false;
     mk::JitShape sh = mk::JIT_STREAM;
     int rc = 0;
-    if (!mk::compile_schedule(h->net, cap, soo != 0, lim, P, w) || !mk::jit_lane_source(P, jl, src, w, &sh)) {
+    if (!mk::compile_schedule(h->net, cap, soo != 0, lim, P, w) || !mk::jit_lane_source(P, jl, src, w, &sh, nullptr, nullptr, true)) {
         src = w;
         rc = 1;
     }

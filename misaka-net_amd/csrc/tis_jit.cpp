@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mk.h"
@@ -84,6 +85,7 @@ struct Graph {
     size_t nreach = 0, ndops = 0; // ndops: micro-ops emitted (rolled runs count once)
     bool cyclic = false;
     std::vector<std::vector<Run>> runs; // per variant, ascending start
+    const JitLimits *lim = nullptr;
 };
 
 bool slot_op(const DOp &I) { return I.op == U_ST || I.op == U_LD || I.op == U_STI; }
@@ -181,6 +183,7 @@ size_t emitted_ops(const std::vector<Run> &runs, size_t lo, size_t hi)
 
 bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string &why)
 {
+    g.lim = &lim;
     g.D = assemble_device(p, 8, g.entry);
     const size_t nv = g.entry.size();
     if (nv == 0) {
@@ -383,23 +386,18 @@ struct OpWriter {
 // A rolled loop whose body only reads stack slots (a run of POPs: LD ops, no
 // ST) is software-pipelined: while one block of U iterations uses its
 // popped values, the slots of the next block are already being read, so a
-// wave keeps ~kPrefetchLoads spill reads in flight instead of draining its
+// wave keeps ~lim.prefetch spill reads in flight instead of draining its
 // loads at every unrolled step (C4's pop loops are a serial ACC chain over
 // the popped values).  Two register sets (A, B) alternate, so no value is
 // copied while its load is in flight (a copy would need the load's wait).
 // Reading ahead is safe because nothing in the loop writes a slot.  Returns
 // false (nothing emitted) for other runs.
-constexpr size_t kPrefetchLoads = 16;
-
 template <class Expr, class RoundEnd>
 bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::vector<const Run *> &outer,
                          const Expr &expr, RoundEnd &round_end)
 {
-    // stream shapes only (the machine shape, whose lane registers live in a
-    // struct, L.r*, was checked bit-exact with it but not measured)
-    if (!r.inner.empty() || std::strcmp(w.R, "r") != 0) return false;
-    size_t depth = kPrefetchLoads; // MK_JIT_PREFETCH=<loads in flight>, 0 = off (experiments)
-    if (const char *env = std::getenv("MK_JIT_PREFETCH"); env && *env) depth = (size_t)std::strtoull(env, nullptr, 10);
+    if (!r.inner.empty()) return false;
+    const size_t depth = g.lim->prefetch; // loads in flight, 0 = off (MK_JIT_PREFETCH)
     if (!depth) return false;
     std::vector<size_t> lds;
     for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
@@ -432,7 +430,7 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
             for (size_t pc = r.start, a = 0; pc < r.start + r.period; ++pc) {
                 const DOp &I = g.D[pc];
                 if (I.op == U_LD) e.line("    %s%u = (int64_t)%c%zu_%zu_%zu;", w.R, I.d / 8, set, D, a++, k);
-                else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+                else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str(), pc);
                 else w.data(I);
             }
             e.line("    }");
@@ -455,7 +453,7 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
         for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
             const DOp &I = g.D[pc];
             if (slot_op(I)) w.data(I, expr(pc, advancing(I)).c_str());
-            else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+            else if (I.op == U_ROUND_END) round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str(), pc);
             else w.data(I);
         }
         e.line("    }");
@@ -469,7 +467,8 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
 // rolling `runs` into nested for loops (loop variables j0, j1, ...); an
 // op's slot or step count is its value in the first copy plus, per
 // enclosing loop, that loop's variable times the op's advance.
-// `round_end(I, inc)` prints a ROUND_END whose step count is the expression `inc`.
+// `round_end(I, inc, pc)` prints a ROUND_END (at pc of the first copy) whose
+// step count is the expression `inc`.
 template <class RoundEnd>
 void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs, size_t lo, size_t hi,
                  std::vector<const Run *> &outer, RoundEnd &round_end)
@@ -503,7 +502,7 @@ void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs
         if (slot_op(I)) {
             w.data(I, expr(pc, advancing(I)).c_str());
         } else if (I.op == U_ROUND_END) {
-            round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str());
+            round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str(), pc);
         } else {
             w.data(I);
         }
@@ -516,6 +515,132 @@ void emit_body(const OpWriter &w, const Graph &g, uint32_t v, size_t lo, size_t 
 {
     std::vector<const Run *> outer;
     emit_rolled(w, g, g.runs[v], lo, hi, outer, round_end);
+}
+
+// ---- budget exits of checked variants ----------------------------------------
+// A checked variant is entered only through its fast variant's GUARD, which
+// fires when steps + (largest round-end count inside) >= budget: every lane
+// in it therefore ends at a round end inside it -- the first round end R
+// whose count inc_R >= budget - steps -- with status BUDGET (plus HAS_OUTPUT
+// if an OUT completed by round R), steps + inc_R, and the /compute output as
+// of round R.  The exit op is never reached.
+//
+// So instead of a test and an early exit per round end (a deep pipeline has
+// thousands: C4 d64's checked variant alone had 5,643, and that CFG took
+// hiprtc minutes), the checked variant runs its whole body -- the same data
+// ops as the fast variant; stack-slot writes past R are harmless because the
+// lane ends -- and then looks R up in the list of its round ends, compressed
+// into arithmetic runs of counts with one status each.  The output value is
+// read once, at the last round end that has one: the schedule compiler sets
+// the output location only at the first OUT (tis_sched.cpp OUTL), so every
+// round end with HAS_OUTPUT sees the same value.
+struct ReSeg {
+    int64_t first = 0, step = 1, last = 0;
+    uint32_t st = 0;
+};
+
+struct RoundEnds {
+    std::vector<ReSeg> segs;
+    size_t snap_pc = SIZE_MAX; // pc (first copy) of the last round end with an output
+};
+
+void collect_round_ends(const Graph &g, const std::vector<Run> &runs, size_t lo, size_t hi,
+                        std::vector<std::pair<const Run *, int64_t>> &outer,
+                        std::vector<std::pair<int64_t, uint32_t>> &out, size_t &snap_pc)
+{
+    size_t ri = 0;
+    for (size_t pc = lo; pc < hi;) {
+        if (ri < runs.size() && runs[ri].start == pc) {
+            const Run &r = runs[ri++];
+            for (size_t j = 0; j < r.reps; ++j) {
+                outer.push_back({&r, (int64_t)j});
+                collect_round_ends(g, r.inner, r.start, r.start + r.period, outer, out, snap_pc);
+                outer.pop_back();
+            }
+            pc += r.reps * r.period;
+            continue;
+        }
+        const DOp &I = g.D[pc];
+        if (I.op == U_ROUND_END) {
+            int64_t inc = I.inc;
+            for (const auto &[o, j] : outer) inc += j * o->delta[pc - o->start];
+            out.push_back({inc, (uint32_t)I.d});
+            if (I.d & MK_ST_HAS_OUTPUT) snap_pc = pc;
+        }
+        ++pc;
+    }
+}
+
+RoundEnds round_ends(const Graph &g, uint32_t v, size_t lo, size_t hi)
+{
+    RoundEnds re;
+    std::vector<std::pair<const Run *, int64_t>> outer;
+    std::vector<std::pair<int64_t, uint32_t>> all;
+    collect_round_ends(g, g.runs[v], lo, hi, outer, all, re.snap_pc);
+    // counts never decrease; of equal counts only the first can be R
+    std::vector<std::pair<int64_t, uint32_t>> u;
+    for (const auto &x : all)
+        if (u.empty() || x.first > u.back().first) u.push_back(x);
+    for (size_t i = 0; i < u.size();) {
+        ReSeg s;
+        s.first = s.last = u[i].first;
+        s.st = u[i].second;
+        size_t k = i + 1;
+        if (k < u.size() && u[k].second == s.st) {
+            s.step = u[k].first - s.first;
+            while (k < u.size() && u[k].second == s.st && u[k].first - s.last == s.step) s.last = u[k++].first;
+        }
+        re.segs.push_back(s);
+        i = k;
+    }
+    return re;
+}
+
+// The lookup after a checked variant's body: sets `inc_` and `st_` (locals
+// declared here) for need = budget - steps (`steps` is the lane's count
+// expression at variant entry).
+void emit_budget_exit(Emitter &e, Emitter &tab, const RoundEnds &re, uint32_t v, const char *steps)
+{
+    e.line("    const int64_t need_ = (int64_t)budget - (int64_t)%s;", steps);
+    e.line("    uint32_t inc_, st_;");
+    auto one = [&](const ReSeg &s, const char *pre) {
+        if (s.first == s.last)
+            e.line("    %s{ inc_ = %lldu; st_ = %uu; }", pre, (long long)s.first, s.st);
+        else
+            e.line("    %s{ inc_ = need_ <= %lldll ? %lldu : (uint32_t)(%lldll + (need_ - %lldll + %lldll) / %lldll * %lldll); "
+                   "st_ = %uu; }",
+                   pre, (long long)s.first, (long long)s.first, (long long)s.first, (long long)s.first,
+                   (long long)(s.step - 1), (long long)s.step, (long long)s.step, s.st);
+    };
+    const size_t n = re.segs.size();
+    if (n <= 8) {
+        for (size_t i = 0; i + 1 < n; ++i) {
+            char pre[64];
+            snprintf(pre, sizeof pre, "%sif (need_ <= %lldll) ", i ? "else " : "", (long long)re.segs[i].last);
+            one(re.segs[i], pre);
+        }
+        one(re.segs[n - 1], n > 1 ? "else " : "");
+        return;
+    }
+    // many segments: binary search over a table {last, first, step, st}
+    std::string t;
+    for (const ReSeg &s : re.segs) {
+        char b[96];
+        snprintf(b, sizeof b, "%lldu,%lldu,%lldu,%uu,", (long long)s.last, (long long)s.first, (long long)s.step, s.st);
+        t += b;
+    }
+    tab.line("MK_CTABLE uint32_t mk_re%u[] = {%s};", v, t.c_str());
+    e.line("    {");
+    e.line("    const uint32_t *re_ = mk_re%u;", v);
+    e.line("    uint32_t lo_ = 0u, hi_ = %zuu;", n - 1);
+    e.line("    while (lo_ < hi_) {");
+    e.line("        const uint32_t m_ = (lo_ + hi_) >> 1;");
+    e.line("        if (need_ <= (int64_t)re_[4u * m_]) hi_ = m_; else lo_ = m_ + 1u;");
+    e.line("    }");
+    e.line("    const int64_t f_ = re_[4u * lo_ + 1u], s_ = re_[4u * lo_ + 2u];");
+    e.line("    inc_ = need_ <= f_ ? (uint32_t)f_ : (uint32_t)(f_ + (need_ - f_ + s_ - 1) / s_ * s_);");
+    e.line("    st_ = re_[4u * lo_ + 3u];");
+    e.line("    }");
 }
 
 // [lo, hi) of variant v's body: after its GUARD, up to its exit op.
@@ -609,6 +734,8 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
     } else {
         live = g.seen;
     }
+    Emitter tab; // budget-exit tables of checked variants (before the function)
+    const size_t fn_start = e.s.size();
     e.line("MK_FN int32_t %s(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,", name);
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
     e.line("{");
@@ -626,14 +753,23 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
             e.line("    if ((uint64_t)steps + %uu >= (uint64_t)budget) goto V%u;", G.inc, (uint32_t)G.imm);
         size_t lo, hi;
         body_range(g, v, lo, hi);
-        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc) {
-            e.line("    if ((uint64_t)steps + %s >= (uint64_t)budget) {", inc);
-            e.line("        steps += (uint32_t)(%s);", inc);
-            e.line("        outv = %s;", w.result(I).c_str());
-            e.line("        st = %uu;", I.d);
-            e.line("        goto done;");
+        const RoundEnds re = round_ends(g, v, lo, hi);
+        if (!re.segs.empty()) { // checked variant: always ends at a round end (emit_budget_exit)
+            e.line("    {");
+            e.line("    int32_t mk_o = 0;");
+            emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
+                if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
+            });
+            emit_budget_exit(e, tab, re, v, "steps");
+            e.line("    steps += inc_;");
+            e.line("    st = st_;");
+            e.line("    outv = (st_ & %uu) ? mk_o : 0;", (unsigned)MK_ST_HAS_OUTPUT);
+            e.line("    (void)mk_o;");
+            e.line("    goto done;");
             e.line("    }");
-        });
+            continue;
+        }
+        emit_body(w, g, v, lo, hi, [&](const DOp &, const char *, size_t) {});
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -674,33 +810,27 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
     e.line("    *status_out = st;");
     e.line("    return outv;");
     e.line("}");
+    e.s.insert(fn_start, tab.s);
 }
 
 // The kernel runs only launches whose budget exceeds every path
 // (MK_MAX_STEPS): its lane function has no guards and no checked variants.
 // The guarded lane (MK_LANE_CHECKED) is for the CPU tests; the executor
 // gives launches with a smaller budget to tier 2.
-// Stream lanes with more micro-ops than this run in the heavy kernel
-// (kJitHeavyOps; MK_JIT_HEAVY_OPS overrides it for tests and tuning).
-size_t jit_heavy_ops()
-{
-    const char *env = std::getenv("MK_JIT_HEAVY_OPS");
-    return env && *env ? (size_t)std::strtoull(env, nullptr, 10) : kJitHeavyOps;
-}
-
-void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps)
+// Stream lanes with more than lim.heavy_ops micro-ops run in the heavy kernel.
+void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps, bool checked)
 {
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 0");
+    e.line("#ifndef MK_CTABLE");
+    e.line("#define MK_CTABLE static const");
+    e.line("#endif");
     e.line("#define MK_MAX_STEPS %lluull", (unsigned long long)max_steps);
     e.line("#define MK_NSLOTS %uu", p.nslots);
     // MK_JIT_SLOT_LAYOUT=blocked|lane overrides the choice (tests, tuning)
-    const char *lay = std::getenv("MK_JIT_SLOT_LAYOUT");
-    const bool blocked = lay && !std::strcmp(lay, "blocked") ? true
-                         : lay && !std::strcmp(lay, "lane") ? false
-                                                             : p.nslots <= kJitWaveBlockedSlots;
+    const bool blocked = g.lim->slot_layout >= 0 ? g.lim->slot_layout == 1 : p.nslots <= kJitWaveBlockedSlots;
     e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
-    if (blocked && g.ndops > jit_heavy_ops()) {
+    if (blocked && g.ndops > g.lim->heavy_ops) {
         // Heavy kernel, wave-blocked: `slots` is the wave's block (wave-uniform)
         // and a slot access is a buffer op whose slot offset s * 256 is a
         // scalar (SGPR + immediate) and whose lane offset is one VGPR, so no
@@ -721,9 +851,11 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("    ((int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0))");
         e.line("#endif");
     }
-    e.line("#ifdef MK_LANE_CHECKED");
-    emit_stream_lane(p, g, e, "mk_lane", false);
-    e.line("#endif");
+    if (checked) { // host tests only: the GPU kernel serves unguarded launches
+        e.line("#ifdef MK_LANE_CHECKED");
+        emit_stream_lane(p, g, e, "mk_lane", false);
+        e.line("#endif");
+    }
     emit_stream_lane(p, g, e, "mk_lane_ng", true);
 }
 
@@ -889,8 +1021,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         e.line("    }");
     };
     int uf = fast_unroll(xpc - gpc - 1);
-    if (const char *env = std::getenv("MK_JIT_LOOP_UNROLL")) // experiments
-        if (std::atoi(env) >= 1 && std::atoi(env) <= 64) uf = std::atoi(env);
+    if (g.lim->loop_unroll >= 1 && g.lim->loop_unroll <= 64) uf = g.lim->loop_unroll; // MK_JIT_LOOP_UNROLL
     // an unguarded phase: chunks of uf iterations while T allows
     auto phase = [&](LoopMode mode, const char *cap) {
         e.line("    while (more && %s - it >= %uu) {", cap, uf);
@@ -978,6 +1109,9 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     std::vector<uint32_t> loops;
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 1");
+    e.line("#ifndef MK_CTABLE");
+    e.line("#define MK_CTABLE static const");
+    e.line("#endif");
     e.line("#define MK_SB_DONE 0xFFFFFFFEu");
     e.line("#define MK_SB_IDLE 0xFFFFFFFFu");
     e.line("struct MkLane {");
@@ -1002,6 +1136,8 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // smax: at least the steps of every lane of the group (self-loops size
     // their unguarded phase from it; the kernel reduces it over the wave for
     // loop variants only, see mk_is_loop).
+    Emitter tab; // budget-exit tables of checked variants (before mk_run)
+    const size_t fn_start = e.s.size();
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
     e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
     e.line("{");
@@ -1026,15 +1162,24 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         }
         size_t lo, hi;
         body_range(g, v, lo, hi);
-        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc) {
-            e.line("    if ((uint64_t)L.steps + %s >= (uint64_t)budget) {", inc);
-            e.line("        L.steps += (uint32_t)(%s);", inc);
-            e.line("        L.outv = %s;", w.result(I).c_str());
-            e.line("        L.st = %uu;", I.d);
-            e.line("        L.sb = MK_SB_DONE;");
-            e.line("        goto X%u;", v);
+        const RoundEnds re = round_ends(g, v, lo, hi);
+        if (!re.segs.empty()) { // checked variant: always ends at a round end (emit_budget_exit)
+            e.line("    int32_t mk_o = 0;");
+            emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
+                if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
+            });
+            emit_budget_exit(e, tab, re, v, "L.steps");
+            e.line("    L.steps += inc_;");
+            e.line("    L.st = st_;");
+            e.line("    L.outv = (st_ & %uu) ? mk_o : 0;", (unsigned)MK_ST_HAS_OUTPUT);
+            e.line("    L.sb = MK_SB_DONE;");
+            e.line("    (void)mk_o;");
+            e.line("    X%u:", v);
+            e.line("    break;");
             e.line("    }");
-        });
+            continue;
+        }
+        emit_body(w, g, v, lo, hi, [&](const DOp &, const char *, size_t) {});
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -1078,6 +1223,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    default: L.sb = MK_SB_DONE; break;");
     e.line("    }");
     e.line("}");
+    e.s.insert(fn_start, tab.s);
     e.line("// %zu self-loops", loops.size());
     e.line("MK_FN bool mk_is_loop(const uint32_t u)");
     e.line("{");
@@ -1108,7 +1254,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 } // namespace
 
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
-                     uint64_t *max_steps, bool *heavy)
+                     uint64_t *max_steps, bool *heavy, bool checked)
 {
     Graph g;
     if (!analyze(p, lim, g, why)) return false;
@@ -1117,10 +1263,10 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else
-        emit_stream(p, g, e, max_fast_steps(p, g));
+        emit_stream(p, g, e, max_fast_steps(p, g), checked);
     if (shape) *shape = s;
     if (max_steps) *max_steps = s == JIT_STREAM ? max_fast_steps(p, g) : UINT64_MAX;
-    if (heavy) *heavy = g.ndops > jit_heavy_ops();
+    if (heavy) *heavy = g.ndops > lim.heavy_ops;
     src = std::move(e.s);
     return true;
 }
@@ -1291,7 +1437,53 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 }
 )";
 
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, uint32_t policy)
+JitLimits JitLimits::from_env()
+{
+    JitLimits l;
+    auto num = [](const char *name, auto &v) {
+        const char *s = std::getenv(name);
+        if (s && *s) v = (std::remove_reference_t<decltype(v)>)std::strtoull(s, nullptr, 10);
+    };
+    auto flag = [](const char *name, bool &v) {
+        const char *s = std::getenv(name);
+        if (s && *s) v = s[0] == '1';
+    };
+    if (const char *s = std::getenv("MK_JIT"); s && !std::strcmp(s, "0")) l.disabled = true;
+    if (const char *s = std::getenv("MK_JIT_SHAPE")) {
+        l.force_machine = !std::strcmp(s, "machine");
+        l.force_stream = !std::strcmp(s, "stream");
+    }
+    if (const char *s = std::getenv("MK_JIT_POLICY")) {
+        unsigned r = 0, nu = 0, mi = 0;
+        if (std::sscanf(s, "%u,%u,%u", &r, &nu, &mi) == 3 && r <= 64 && nu <= 16 && mi <= 64)
+            l.policy = r | nu << 8 | mi << 16;
+    }
+    if (const char *s = std::getenv("MK_JIT_SLOT_LAYOUT"))
+        l.slot_layout = !std::strcmp(s, "blocked") ? 1 : !std::strcmp(s, "lane") ? 0 : -1;
+    if (const char *s = std::getenv("MK_JIT_COMPILE_S"); s && *s) l.max_compile_s = std::strtod(s, nullptr);
+    num("MK_JIT_MAX_DOPS", l.max_dops);
+    num("MK_JIT_MAX_SRC", l.max_src_bytes);
+    num("MK_JIT_LOOP_UNROLL", l.loop_unroll);
+    num("MK_JIT_PREFETCH", l.prefetch);
+    num("MK_JIT_HEAVY_OPS", l.heavy_ops);
+    num("MK_JIT_SLOT_BYTES", l.slot_bytes);
+    if (!l.slot_bytes) l.slot_bytes = kJitSlotBytes;
+    flag("MK_JIT_SLOT_NT", l.slot_nt);
+    flag("MK_JIT_IO_NT", l.io_nt);
+    flag("MK_JIT_COMPACT", l.compact);
+    return l;
+}
+
+std::string JitLimits::key() const
+{
+    char b[256];
+    snprintf(b, sizeof b, "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,compact=%d",
+             force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
+             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, (int)compact);
+    return b;
+}
+
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim)
 {
     Emitter e;
     // hiprtc declares the fixed-width integer types in __hip_internal only
@@ -1313,9 +1505,10 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_ST_STACK_OVERFLOW %d", MK_ST_STACK_OVERFLOW);
     e.line("#define MK_ST_OUTPUT_STOP %d", MK_ST_OUTPUT_STOP);
     e.line("#define MK_FN static __device__ __forceinline__");
+    e.line("#define MK_CTABLE static __device__ const");
     // machine-shape policy word, a constant of the module so that the loop
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
-    e.line("#define MK_POLICY 0x%08xu", policy);
+    e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks
@@ -1333,7 +1526,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_FLAG_NZ(x) mk_flag_nz(x)");
     e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
-    if (const char *nt = std::getenv("MK_JIT_SLOT_NT"); nt && nt[0] == '1') {
+    if (lim.slot_nt) {
         e.line("#define MK_SLOT_ST(b, ss, s, v) __builtin_nontemporal_store((v), (b) + (uint64_t)(s) * (ss))");
         e.line("#define MK_SLOT_LD(b, ss, s) __builtin_nontemporal_load((b) + (uint64_t)(s) * (ss))");
     } else {
@@ -1342,7 +1535,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     }
     // vector out/status stores of the light stream kernel (MK_JIT_IO_NT=1: non-temporal, experiments)
     e.line("typedef int32_t mk_i32x4 __attribute__((ext_vector_type(4)));");
-    if (const char *nt = std::getenv("MK_JIT_IO_NT"); nt && nt[0] == '1')
+    if (lim.io_nt)
         e.line("#define MK_IO_ST(ptr, v) __builtin_nontemporal_store((v), (ptr))");
     else
         e.line("#define MK_IO_ST(ptr, v) (*(ptr) = (v))");

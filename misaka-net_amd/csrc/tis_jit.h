@@ -22,17 +22,61 @@
 
 namespace mk {
 
+enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
+
+constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane per thread
+// Heavy kernels run one thread per input; a launch covers at most as many
+// inputs as fit this much stack-slot memory (more take several launches).
+constexpr size_t kJitSlotBytes = size_t(16) << 30;
+// Default machine-shape policy word (kMachineKernel): generations -- a wave
+// refills only once all its lanes have ended and loops never leave early.
+// Measured on MI355X (C5): ahead of every early-refill / early-leave setting
+// tried (refill 1..48 lanes, leave at 8..14/16), whose extra dispatches and
+// small groups cost more than the idle lanes they save.
+constexpr uint32_t kJitPolicy = 64u | (0u << 8) | (64u << 16);
+// POP loops keep this many slot reads in flight (emit_prefetched_run).
+constexpr size_t kJitPrefetchLoads = 16;
+
+// Limits and code-shape knobs of the native tier.  The defaults are the
+// product; from_env() overlays the MK_JIT_* experiment variables.  A loaded
+// network takes one snapshot at mk_net_load, so every module it compiles,
+// every plan it reports and every launch it makes use the same knobs (a
+// later change of the environment affects networks loaded after it).
 struct JitLimits {
     uint32_t max_variants = 4096; // superblock variants (labels)
     size_t max_dops = 4096;       // micro-ops emitted, after rolling repeats into loops
                                   // (hiprtc time grows superlinearly: 14K straight-line
                                   // ops take ~150 s)
     size_t max_scan = 1u << 22;   // micro-ops of reachable code scanned before giving up
-    bool force_machine = false;   // machine shape even for acyclic graphs (tests)
-    bool force_stream = false;    // stream shape even for cyclic graphs (experiments)
-};
+    // Bound on the generated lane source handed to hiprtc (bytes, without the
+    // host-only checked variant).  Compile time follows the size of the
+    // function LLVM sees; past this the network stays on tier 2 with the
+    // reason in mk_net_plan (MK_JIT_MAX_SRC).
+    size_t max_src_bytes = size_t(1) << 20;
+    // Wall-clock bound on one hiprtc compilation (seconds, MK_JIT_COMPILE_S):
+    // the compile runs on a helper thread, and when it does not finish in
+    // time the network stays on tier 2 (the compile is left to finish in the
+    // background and its result discarded).
+    double max_compile_s = 60.0;
+    bool disabled = false;      // MK_JIT=0: no native tier
+    bool force_machine = false; // MK_JIT_SHAPE=machine: machine shape even for acyclic graphs (tests)
+    bool force_stream = false;  // MK_JIT_SHAPE=stream: stream shape even for cyclic graphs (experiments)
+    uint32_t policy = kJitPolicy;          // MK_JIT_POLICY=refill,num,min
+    int loop_unroll = 0;                   // MK_JIT_LOOP_UNROLL (0: by body size, fast_unroll)
+    int slot_layout = -1;                  // MK_JIT_SLOT_LAYOUT=blocked(1)|lane(0); -1: by size
+    bool slot_nt = false;                  // MK_JIT_SLOT_NT=1: non-temporal slot accesses
+    bool io_nt = false;                    // MK_JIT_IO_NT=1: non-temporal out/status stores
+    size_t prefetch = kJitPrefetchLoads;   // MK_JIT_PREFETCH (0: off)
+    size_t heavy_ops = kJitHeavyOps;       // MK_JIT_HEAVY_OPS
+    uint64_t slot_bytes = kJitSlotBytes;   // MK_JIT_SLOT_BYTES
+    // Compaction of divergent self-loops in the machine shape (MK_JIT_COMPACT=0 off).
+    bool compact = true;
 
-enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
+    static JitLimits from_env();
+    // The knobs that change generated code, as text (the module cache key
+    // and the `knobs=` field of mk_net_plan).
+    std::string key() const;
+};
 
 // The lane source for `p` in portable C++ (host g++ or HIP device).  Both
 // shapes define
@@ -45,26 +89,25 @@ enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
 // Returns false (why) when over limits.
 // max_steps: the stream shape's longest path in retired instructions (its
 // kernel serves launches with a larger budget only); UINT64_MAX for machine.
-// heavy: more than kJitHeavyOps micro-ops emitted (the stream shape then
+// heavy: more than lim.heavy_ops micro-ops emitted (the stream shape then
 // runs one lane per thread in 64-thread blocks instead of 4-lane tiles).
+// The checked lane (mk_lane of the stream shape) is emitted only with
+// `checked` (host tests); the GPU module does not compile it.
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why,
-                     JitShape *shape = nullptr, uint64_t *max_steps = nullptr, bool *heavy = nullptr);
+                     JitShape *shape = nullptr, uint64_t *max_steps = nullptr, bool *heavy = nullptr,
+                     bool checked = false);
 
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of
 // the given shape.
-// policy: the machine shape's policy word (kJitPolicy), compiled in.
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, uint32_t policy);
+// lim.policy (the machine shape's policy word) is compiled in.
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim);
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
-constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane per thread
 constexpr int kJitHeavyBlock = 64;
-// Heavy kernels run one thread per input; a launch covers at most as many
-// inputs as fit this much stack-slot memory (more take several launches).
-constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // Heavy-kernel slot layout: up to this many slots per lane, wave-blocked
 // ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, read
 // and written by buffer ops whose slot offset s * 256 is a scalar, which
@@ -75,12 +118,5 @@ constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // the buffer ops, blocked held 116 VGPRs and lost: 4.14 vs 3.42 ms).
 // MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
 constexpr uint32_t kJitWaveBlockedSlots = 1u << 22;
-
-// Default machine-shape policy word (kMachineKernel): generations -- a wave
-// refills only once all its lanes have ended and loops never leave early.
-// Measured on MI355X (C5): ahead of every early-refill / early-leave setting
-// tried (refill 1..48 lanes, leave at 8..14/16), whose extra dispatches and
-// small groups cost more than the idle lanes they save.
-constexpr uint32_t kJitPolicy = 64u | (0u << 8) | (64u << 16);
 
 } // namespace mk

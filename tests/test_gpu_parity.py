@@ -141,18 +141,19 @@ def test_heavy_kernel_pops_sign_extend(gpu, monkeypatch, layout, depth):
     assert_same(net.compute_batch(xs), ref, f"signed pops D={depth} {layout}")
 
 
-# Pipelined POP loops (emit_prefetched_run: reps >= 64) in both stream
-# kernels: the light one (4 lanes per thread, lane-major slots) and the heavy
-# one (wave-blocked buffer slots); the machine shape keeps plain loops.  The
-# 8-node pipeline is not forced onto the machine shape: that module is 1.8 MB
-# and hiprtc takes minutes over it.
+# Pipelined POP loops (emit_prefetched_run: reps >= 64) in every kernel: the
+# light stream one (4 lanes per thread, lane-major slots), the heavy one
+# (wave-blocked buffer slots) and the machine shape (lane registers in a
+# struct).  The 8-node pipeline on the machine shape used to be a 1.4 MB
+# module that took hiprtc minutes (one early exit per round end in its
+# checked variant); with the budget-exit lookup it compiles in seconds.
 @pytest.mark.parametrize("shape", ["light", "heavy", "machine"])
 def test_pipelined_pops_every_shape(gpu, monkeypatch, shape):
     if shape == "heavy":
         monkeypatch.setenv("MK_JIT_HEAVY_OPS", "16")
     if shape == "machine":
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
-    cases = [signed_pop_network(300)] + ([] if shape == "machine" else [mk.networks.pipeline_network(256)])
+    cases = [signed_pop_network(300), mk.networks.pipeline_network(256)]
     for nodes in cases:
         net = mk.Network(nodes)
         plan = net.plan()
@@ -379,6 +380,28 @@ def test_c4_full_size_properties(gpu):
     ref = oracle(nodes, po.gen_inputs(SEED, n)[sl])
     assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
     assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
+
+
+# The other two C4 bench workloads at their bench sizes, through the default
+# heavy kernel (wave-blocked buffer slots: d256 1,864 slots x 8,192 waves,
+# d1024 8,008 slots x 4,096 waves = 8.4 GB): constant status and steps on
+# every lane (the pipeline's control flow does not depend on x), the
+# counters, and a tail slice bit-exact against the oracle
+# (stack.go:95-155, intStack.go:20-38).
+@pytest.mark.parametrize("depth,n,tail", [(256, 1 << 19, 2048), (1024, 1 << 18, 512)])
+def test_c4_deep_full_size_properties(gpu, depth, n, tail):
+    nodes = mk.networks.pipeline_network(depth)
+    net = mk.Network(nodes)
+    assert "shape=stream-heavy" in net.plan(), net.plan()
+    out, st, sp, stats = _device_run(net, n)
+    sl = slice(n - tail, n)
+    ref = oracle(nodes, po.gen_inputs(SEED, n)[sl])
+    assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
+    assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
+    # every lane's output is a function of its own input only: equal inputs, equal outputs
+    xs = po.gen_inputs(SEED, n)
+    head = oracle(nodes, xs[:tail])
+    assert np.array_equal(out[:tail], head[0])
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -162,3 +162,47 @@ def test_module_compiles_for_gfx950(which, io_nt, monkeypatch):
     assert plan.startswith("tier=native "), plan
     src = net.jit_source()
     assert "mk_jit_exec" in src and "mk_lane" in src
+
+
+# The machine shape of the deep pipelines (C4) used to hand hiprtc a 1.4 MB
+# function whose checked variant had one early exit per round end (5,643 at
+# D=64); it now looks the budget exit up after the body (tis_jit.cpp
+# emit_budget_exit) and every C4 depth compiles well inside the bound, with
+# the pipelined POP loops on.
+COMPILE_BOUND_S = 60
+
+
+@pytest.mark.parametrize("depth", [64, 256, 1024])
+def test_machine_shape_pipeline_compiles_in_bound(depth, monkeypatch):
+    monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+    net = mk.Network(mk.networks.pipeline_network(depth))
+    plan = net.plan(mode="jit")
+    assert plan.startswith("tier=native ") and "shape=machine" in plan, plan
+    secs = float(plan.split("compile=")[1].split("s")[0])
+    assert secs < COMPILE_BOUND_S, plan
+    src = net.jit_source()
+    assert len(src) < (1 << 20) and "mk_jit_exec" in src
+
+
+def test_compile_bounds_fall_back_with_reason(monkeypatch):
+    # over the source bound: tier 2 runs it, mk_net_plan names the bound
+    monkeypatch.setenv("MK_JIT_MAX_SRC", "1000")
+    net = mk.Network(mk.networks.pipeline_network(64))
+    plan = net.plan()
+    assert plan.startswith("tier=compiled ") and "compile bound" in plan, plan
+    assert mk.Network(mk.networks.pipeline_network(64)).plan(mode="jit").startswith("tier=none"), plan
+    # over the time bound: the compile is abandoned, tier 2 runs it
+    monkeypatch.delenv("MK_JIT_MAX_SRC")
+    monkeypatch.setenv("MK_JIT_COMPILE_S", "0.001")
+    plan = mk.Network(mk.networks.pipeline_network(256)).plan()
+    assert plan.startswith("tier=compiled ") and "did not finish" in plan, plan
+
+
+def test_knobs_are_snapshotted_per_network(monkeypatch):
+    # a network keeps the knobs of its load: plan, source and module agree
+    monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+    net = mk.Network(mk.networks.example_network())
+    monkeypatch.setenv("MK_JIT_SHAPE", "stream")
+    assert "shape=machine" in net.plan(mode="jit")
+    assert "#define MK_JIT_MACHINE 1" in net.jit_source()
+    assert "knobs=shape=machine" in net.plan(mode="jit")
