@@ -166,6 +166,16 @@ int mk_session_create(mk_net *net, int device, size_t n, const mk_opts *opts, mk
 /* One /compute call on every session (host arrays; synchronous). */
 int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps);
 
+/* ncalls sequential /compute calls on every session in one launch (host
+ * arrays laid out [call][session]; synchronous): call c of session i takes
+ * in[c*n + i] and reports out/status/steps[c*n + i], exactly as ncalls
+ * mk_session_compute calls in a row would.  Replaces a burst of concurrent
+ * /compute requests on the reference's one network (master.go:197-224 served
+ * one at a time through inChan/outChan, :216-219); the master coalesces such
+ * bursts into one call (misaka_net_amd.master). */
+int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
+                           uint32_t *steps);
+
 /* The same on device arrays, asynchronous on `stream` (NULL = the session's
  * own stream); calls on one session are ordered. */
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,

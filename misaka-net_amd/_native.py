@@ -105,6 +105,7 @@ SIGNATURES = {
     "mk_stats_fold": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "mk_session_create": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(mk_opts), C.POINTER(C.c_void_p)]),
     "mk_session_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mk_session_compute_seq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_compute_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_reset": (C.c_int, [C.c_void_p]),
     "mk_session_free": (None, [C.c_void_p]),

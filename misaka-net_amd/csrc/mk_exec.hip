@@ -795,10 +795,11 @@ struct SessParams {
     uint64_t n;         // sessions
     uint32_t budget;    // retired instructions per call
     uint32_t stack_cap;
-    const int64_t *in;  // [n] this call's inputs (strconv.Atoi values)
-    int32_t *out;       // [n]
-    uint8_t *status;    // [n]
-    uint32_t *steps;    // [n] or null
+    uint32_t ncalls;    // sequential /compute calls per session in this launch
+    const int64_t *in;  // [ncalls][n] the calls' inputs (strconv.Atoi values)
+    int32_t *out;       // [ncalls][n]
+    uint8_t *status;    // [ncalls][n]
+    uint32_t *steps;    // [ncalls][n] or null
     int64_t *acc, *bak; // [nprog][n]
     int32_t *ip, *pendv;  // [nprog][n]
     int32_t *port;      // [nprog*4][n]
@@ -848,7 +849,11 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     }
     bool in_full = io & 1u, out_full = (io >> 1) & 1u;
     uint32_t dead = (io >> 4) & 15u;
-    const int32_t x = live ? (int32_t)p.in[gid] : 0; // int32(v) at GetInput (master.go:237)
+    // ncalls sequential /compute calls, the state carried in registers/LDS
+    // from one to the next (a burst of requests on one instance, one launch)
+    for (uint32_t call = 0; call < p.ncalls; ++call) {
+    const uint64_t ci = (uint64_t)call * n + gid;
+    const int32_t x = live ? (int32_t)p.in[ci] : 0; // int32(v) at GetInput (master.go:237)
     bool active = live && dead == 0, deposited = false, got = false;
     int32_t result = 0;
     uint32_t steps = 0;
@@ -1008,6 +1013,12 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
             }
         }
     }
+    if (live) {
+        p.out[ci] = got ? result : 0;
+        p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : dead);
+        if (p.steps) p.steps[ci] = steps;
+    }
+    } // calls
 
     if (!live) return;
 #pragma unroll
@@ -1025,9 +1036,6 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (dead << 4);
     p.in_val[gid] = in_val;
     p.out_val[gid] = out_val;
-    p.out[gid] = got ? result : 0;
-    p.status[gid] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : dead);
-    if (p.steps) p.steps[gid] = steps;
 }
 
 __global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
@@ -1736,6 +1744,8 @@ struct mk_session {
     void *d_state = nullptr; // every per-session array, one allocation
     size_t state_bytes = 0;
     void *d_stage = nullptr; // host-API staging: in, out, status, steps
+    void *h_stage = nullptr; // pinned host mirror of d_stage
+    size_t stage_bytes = 0;
     hipStream_t stream = nullptr;
     mk::SessParams p{};
     ~mk_session()
@@ -1744,6 +1754,7 @@ struct mk_session {
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipFree(d_state);
         (void)hipFree(d_stage);
+        (void)hipHostFree(h_stage);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -1752,10 +1763,11 @@ namespace mk {
 namespace {
 
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
-                   hipStream_t stream)
+                   hipStream_t stream, uint32_t ncalls = 1)
 {
-    if (s->n == 0) return MK_OK;
+    if (s->n == 0 || ncalls == 0) return MK_OK;
     SessParams p = s->p;
+    p.ncalls = ncalls;
     p.in = d_in;
     p.out = d_out;
     p.status = d_status;
@@ -1999,29 +2011,52 @@ int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out
     return MK_OK;
 }
 
-int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps)
+int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
+                           uint32_t *steps)
 {
-    if (!s || (s->n && (!in || !out || !status))) return MK_EINVAL;
-    if (s->n == 0) return MK_OK;
+    if (!s || (s->n && ncalls && (!in || !out || !status))) return MK_EINVAL;
+    if (s->n == 0 || ncalls == 0) return MK_OK;
+    if (ncalls > 0xffffffffull) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
-    const size_t n = s->n;
-    const size_t a8 = (n * 8 + 255) & ~(size_t)255, a4 = (n * 4 + 255) & ~(size_t)255;
-    if (!s->d_stage && hipMalloc(&s->d_stage, a8 + a4 + a4 + n) != hipSuccess) return MK_ENOMEM;
-    char *b = (char *)s->d_stage;
+    const size_t m = s->n * ncalls;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t a8 = al(m * 8), a4 = al(m * 4), need = a8 + a4 + a4 + al(m);
+    // device buffers plus a pinned host mirror (small bursts are latency-bound:
+    // pinned copies avoid the runtime's pageable staging and its extra sync)
+    if (need > s->stage_bytes) {
+        (void)hipFree(s->d_stage);
+        (void)hipHostFree(s->h_stage);
+        s->d_stage = s->h_stage = nullptr;
+        s->stage_bytes = 0;
+        if (hipMalloc(&s->d_stage, need) != hipSuccess) return MK_ENOMEM;
+        if (hipHostMalloc(&s->h_stage, need, hipHostMallocDefault) != hipSuccess) return MK_ENOMEM;
+        s->stage_bytes = need;
+    }
+    char *b = (char *)s->d_stage, *hb = (char *)s->h_stage;
     int64_t *din = (int64_t *)b;
     int32_t *dout = (int32_t *)(b + a8);
     uint32_t *dsteps = (uint32_t *)(b + a8 + a4);
     uint8_t *dst = (uint8_t *)(b + a8 + a4 + a4);
-    if (hipMemcpyAsync(din, in, n * 8, hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
-    int rc = mk::session_launch(s, din, dout, dst, steps ? dsteps : nullptr, s->stream);
+    memcpy(hb, in, m * 8);
+    if (hipMemcpyAsync(din, hb, m * 8, hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
+    int rc = mk::session_launch(s, din, dout, dst, steps ? dsteps : nullptr, s->stream, (uint32_t)ncalls);
     if (rc) return rc;
-    if (hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-        hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+    if (hipMemcpyAsync(hb + a8, dout, m * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+        hipMemcpyAsync(hb + a8 + a4 + a4, dst, m, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
         return MK_EDEVICE;
-    if (steps && hipMemcpyAsync(steps, dsteps, n * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+    if (steps && hipMemcpyAsync(hb + a8 + a4, dsteps, m * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
         return MK_EDEVICE;
-    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
+    memcpy(out, hb + a8, m * 4);
+    memcpy(status, hb + a8 + a4 + a4, m);
+    if (steps) memcpy(steps, hb + a8 + a4, m * 4);
+    return MK_OK;
+}
+
+int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps)
+{
+    return mk_session_compute_seq(s, in, 1, out, status, steps);
 }
 
 void mk_session_free(mk_session *s) { delete s; }

@@ -17,11 +17,18 @@ Deliberate differences (DESIGN.md / INTEGRATION.md):
     program nodes serve :8001, master.go:178, so its /load never completes);
     a rejected program answers 400 "error loading program on node X: <Go
     error text>" and leaves the previous program in place (program.go:180-192).
-  * by default every /compute runs on a fresh post-/reset copy of the network
-    (the lane model: independent inputs, batchable).  ``stateful=True`` keeps
-    the reference's semantics instead (row f2): one network instance whose
-    node state, stacks and channels persist across /compute calls, on the GPU
-    (SessionSet); /reset and /load reset it, /pause keeps it.
+  * by default (``stateful=True``) the reference's semantics: one network
+    instance whose node state, stacks and channels persist across /compute
+    calls (program.go:80-92, master.go:216-219), on the GPU (SessionSet, row
+    f2); /reset and /load reset it, /pause keeps it.  Concurrent /compute
+    requests are coalesced: the ones that arrive while a launch is in flight
+    run, in arrival order, as sequential calls of the next single launch
+    (mk_session_compute_seq) -- the reference serves them one at a time
+    through its capacity-1 inChan/outChan.
+  * ``stateful=False`` is the batch extension (the lane model): every input
+    runs on a fresh post-/reset copy of the network, and concurrent /compute
+    requests are coalesced into one mk_compute_batch.  /compute_batch is the
+    explicit many-values form of either mode.
   * ``wire=MasterService`` (misaka_net_amd.wire, row f4): /compute goes over
     the reference's gRPC wire instead -- inChan/outChan served as
     grpc.Master.GetInput/SendOutput to external (reference) program nodes,
@@ -96,6 +103,57 @@ def http_error(msg: str, code: int) -> Response:
     return Response(code, msg + "\n")  # http.Error appends a newline
 
 
+class _Slot:
+    __slots__ = ("v", "done", "result", "error")
+
+    def __init__(self, v):
+        self.v, self.done, self.result, self.error = v, False, None, None
+
+
+class Coalescer:
+    """Group commit for concurrent single-value requests: a request that finds
+    no batch in flight runs every request queued so far (``max_batch`` at a
+    time) as one ``run(values) -> [(has_output, value)]`` call; requests that
+    arrive meanwhile wait and form the next batch.  No timer: under load the
+    batch is whatever accumulated during the previous launch, and a lone
+    request runs at once."""
+
+    def __init__(self, run, max_batch: int = 65536):
+        self._run, self.max_batch = run, max_batch
+        self._q: list = []
+        self._cv = threading.Condition()
+        self._busy = False
+        self.batches = 0  # launches made (tests and the bench read it)
+        self.requests = 0
+
+    def submit(self, v):
+        s = _Slot(v)
+        with self._cv:
+            self._q.append(s)
+            while not s.done:
+                if self._busy:
+                    self._cv.wait()
+                    continue
+                self._busy = True
+                batch, self._q = self._q[: self.max_batch], self._q[self.max_batch:]
+                self._cv.release()
+                try:
+                    res, err = self._run([b.v for b in batch]), None
+                except Exception as e:  # delivered to every request of the batch
+                    res, err = None, e
+                finally:
+                    self._cv.acquire()
+                for i, b in enumerate(batch):
+                    b.result, b.error, b.done = (res[i] if res is not None else None), err, True
+                self.batches += 1
+                self.requests += len(batch)
+                self._busy = False
+                self._cv.notify_all()
+        if s.error is not None:
+            raise s.error
+        return s.result
+
+
 class MasterNode:
     """In-process master: the request handlers of master.go over a Network.
 
@@ -105,8 +163,8 @@ class MasterNode:
     """
 
     def __init__(self, node_info: Mapping[str, Mapping], programs: Optional[Mapping[str, str]] = None,
-                 name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = False,
-                 wire=None, wire_timeout: Optional[float] = 30.0):
+                 name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = True,
+                 wire=None, wire_timeout: Optional[float] = 30.0, max_batch: int = 65536):
         self.node_info = {k: dict(v) for k, v in node_info.items()}
         self.name = name
         self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
@@ -126,6 +184,7 @@ class MasterNode:
         self.stateful = stateful
         self._sess = None
         self.wire, self.wire_timeout = wire, wire_timeout
+        self.coalescer = Coalescer(self._run_batch, max_batch)
 
     # -- network handle ------------------------------------------------------
     def _specs(self):
@@ -155,6 +214,18 @@ class MasterNode:
             self._sess.close()
             self._sess = None
 
+    def _run_batch(self, vals):
+        """Values of coalesced requests -> [(has_output, value)] in order: on
+        the one persistent instance as sequential calls (stateful), or as
+        independent lanes (stateless); one executor launch either way."""
+        with self._lock:
+            if self.stateful:
+                r = self.session().compute_seq(np.asarray(vals, dtype=np.int64), steps=False)
+            else:
+                r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
+                                                 stack_cap=self.stack_cap, devices=self.devices, steps=False)
+        return [(bool(int(st) & N.MK_ST_HAS_OUTPUT), int(o)) for o, st in zip(r.out.tolist(), r.status.tolist())]
+
     def _call(self, v: int):
         """One /compute: (has_output, value)."""
         if self.wire is not None:
@@ -162,12 +233,7 @@ class MasterNode:
                 return True, self.wire.compute(v, timeout=self.wire_timeout)
             except Exception:  # timeout or cancelled by /pause, /reset
                 return False, 0
-        if self.stateful:
-            r = self.session().compute([v], steps=False)
-        else:
-            r = self.network().compute_batch([v], budget=self.budget, stack_cap=self.stack_cap,
-                                             devices=self.devices, steps=False)
-        return bool(int(r.status[0]) & N.MK_ST_HAS_OUTPUT), int(r.out[0])
+        return self.coalescer.submit(v)
 
     # -- handlers -------------------------------------------------------------
     def handle(self, method: str, path: str, query: str = "", body: bytes = b"", ctype: str = "") -> Response:
@@ -237,7 +303,13 @@ class MasterNode:
             e = self._check_types()
             if e:
                 return http_error(f"error resetting network: {e}", 400)
-            self.is_running = False  # /load resets the network first (master.go:166-175)
+            # /load resets the whole network before the Load RPC, whatever the
+            # RPC then does (master.go:165-175: broadcast reset, stopNode,
+            # resetNode): node state, stacks and the master's channels
+            self.is_running = False
+            self._drop_state()
+            if self.wire is not None:
+                self.wire.reset()
             if self.node_info[target].get("type") != "program":
                 return http_error(f"error loading program on node {target}: not a program node", 400)
             try:
@@ -245,7 +317,6 @@ class MasterNode:
             except TisParseError as ex:
                 return http_error(f"error loading program on node {target}: {ex}", 400)
             self.programs[target] = program
-            self._drop_state()
             if self._net is not None:
                 self._net.close()
                 self._net = None
@@ -265,11 +336,7 @@ class MasterNode:
             v = go_atoi(self._values(form)[0])
         except ValueError:
             return http_error("cannot parse value", 400)
-        if self.wire is not None:  # concurrent handlers, like net/http (master.go:197)
-            ok, out = self._call(v)
-        else:
-            with self._lock:
-                ok, out = self._call(v)
+        ok, out = self._call(v)  # concurrent handlers, like net/http (master.go:197)
         if not ok:
             return http_error("network produced no output", 504)
         # json.NewEncoder(w).Encode(clientOutResponse{...}) (master.go:219): compact, newline-terminated
@@ -291,10 +358,9 @@ class MasterNode:
         except (ValueError, TypeError, AttributeError):
             return http_error("cannot parse value", 400)
         with self._lock:
-            if self.stateful:  # sequential /compute calls on the one instance
-                res = [self.session().compute([v], steps=False) for v in vals]
-                outs = [int(r.out[0]) for r in res]
-                sts = [int(r.status[0]) for r in res]
+            if self.stateful:  # sequential /compute calls on the one instance, one launch
+                r = self.session().compute_seq(np.asarray(vals, dtype=np.int64), steps=False)
+                outs, sts = r.out.tolist(), r.status.tolist()
             else:
                 r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
                                                  stack_cap=self.stack_cap, devices=self.devices, steps=False)

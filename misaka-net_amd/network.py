@@ -287,6 +287,27 @@ class SessionSet:
                 "mk_session_compute")
         return BatchResult(out, st, sp)
 
+    def compute_seq(self, values, *, steps=True) -> BatchResult:
+        """Sequential /compute calls in one launch: ``values`` has shape
+        (ncalls, n) -- row c is call c on every instance -- or, for n == 1,
+        a flat list of the calls.  Results have the shape of ``values``."""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        shape = v.shape
+        if v.ndim == 1 and self.n == 1:
+            v = v.reshape(-1, 1)
+        if v.ndim != 2 or v.shape[1] != self.n:
+            raise ValueError(f"expected (ncalls, {self.n}) values, got {shape}")
+        m = v.shape[0]
+        out = np.zeros(v.shape, np.int32)
+        st = np.zeros(v.shape, np.uint8)
+        sp = np.zeros(v.shape, np.uint32) if steps else None
+        if m:
+            N.check(N.lib().mk_session_compute_seq(self._h, v.ctypes.data_as(C.c_void_p), m,
+                                                   out.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p),
+                                                   sp.ctypes.data_as(C.c_void_p) if sp is not None else None),
+                    "mk_session_compute_seq")
+        return BatchResult(out.reshape(shape), st.reshape(shape), sp.reshape(shape) if sp is not None else None)
+
     def compute_device(self, in_ptr, out_ptr, status_ptr, steps_ptr=None, *, stream=None):
         N.check(N.lib().mk_session_compute_device(self._h, in_ptr, out_ptr, status_ptr, steps_ptr, stream),
                 "mk_session_compute_device")

@@ -10,7 +10,7 @@ C3     network built around docs/sample.txt "Example 2" (sample.txt:20-29),
        ``//`` comments (MOV R3, ACC / ADD ACC) then OUT ACC.  Zero input ->
        no output (quiescent); otherwise int32(2x).
 C4     8-program-node pipeline; node k pushes D values to its own stack,
-       pops them back folding sum = 4*sum + v (ports used as scratch), and forwards the
+       pops them back folding sum = 3*sum + v (ports used as scratch), and forwards the
        int32 sum to node k+1; the last node outputs.
 C5     data-dependent countdown (``L: SUB 1 / JGZ L``) feeding a JRO-dispatched
        digit loop: trip counts follow the input, lanes diverge.

@@ -512,3 +512,32 @@ def test_sessions_deep_stacks(gpu):
     nodes = mk.networks.pipeline_network(64)
     seqs = po.gen_inputs(SEED, 3 * 500).reshape(3, 500)
     _session_calls(nodes, seqs)
+
+
+# Sequential calls in one launch (mk_session_compute_seq): identical to the
+# same calls made one launch each, and to the oracle's session restatement.
+@pytest.mark.parametrize("seed", range(0, 24))
+def test_session_seq_matches_single_calls(gpu, seed):
+    rows = random_network(seed) if seed else mk.networks.countdown_network()
+    cap = [1, 3, 8, 16, 17, 40, 1024][seed % 7]
+    budget = [37, 200, 1000][seed % 3]
+    seqs = po.gen_inputs(seed * 977 + 3, 7 * 200, kind=1 if not seed else 0, mask=1023).reshape(7, 200)
+    g, o = _session_pair(rows, 200, budget=budget, stack_cap=cap)
+    got = g.compute_seq(seqs)
+    for k, row in enumerate(seqs):
+        ref = o.compute(row, budget=budget, threads=THREADS)
+        assert_same(mk.network.BatchResult(got.out[k], got.status[k], got.steps[k]), ref, f"seq call {k}")
+    # the state after the burst continues like the oracle's
+    row = po.gen_inputs(seed + 11, 200)
+    assert_same(g.compute(row), o.compute(row, budget=budget, threads=THREADS), "after burst")
+
+
+def test_session_seq_single_instance_long_burst(gpu):
+    # the master's stateful mode: one instance, a burst of 4,096 calls
+    nodes = [("acc", "program", "IN ACC\nADD R0\nMOV ACC, acc:R0\nOUT ACC\nMOV R0, ACC\nMOV ACC, acc:R0")]
+    g = mk.Network(nodes).sessions(1)
+    xs = po.gen_inputs(SEED, 4096)
+    r = g.compute_seq(xs)
+    o = po.OracleSessions(po.OracleNet(nodes), 1)
+    ref = [o.compute([x]) for x in xs.tolist()]
+    assert r.out.tolist() == [int(x[0][0]) for x in ref] and r.status.tolist() == [int(x[1][0]) for x in ref]

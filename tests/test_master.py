@@ -4,11 +4,12 @@ The compute paths run on the GPU (marked)."""
 import http.client
 import json
 import threading
+import time
 
 import pytest
 
 import misaka_net_amd as mk
-from misaka_net_amd.master import MasterNode, go_atoi, make_server, parse_query
+from misaka_net_amd.master import Coalescer, MasterNode, go_atoi, make_server, parse_query
 
 NODE_INFO = {"misaka1": {"type": "program"}, "misaka2": {"type": "program"}, "misaka3": {"type": "stack"}}
 PROGRAMS = {"misaka1": mk.networks.EXAMPLE_MISAKA1, "misaka2": mk.networks.EXAMPLE_MISAKA2}
@@ -70,6 +71,83 @@ def test_load_success_and_run_pause_reset():
     for path in ("/run", "/pause", "/reset"):
         assert m.handle("POST", path).body == "Success"
     assert not m.is_running
+
+
+class _FakeSession:
+    def __init__(self):
+        self.closed = False
+
+    def close(self):
+        self.closed = True
+
+
+class _FakeWire:
+    def __init__(self):
+        self.resets = 0
+
+    def reset(self):
+        self.resets += 1
+
+    def cancel(self):
+        pass
+
+
+@pytest.mark.parametrize("program,code", [(b"program=MOV+1%2CACC", 400), (b"program=NOP", 200)])
+def test_load_resets_state_even_when_rejected(program, code):
+    # master.go:165-175 resets every node and the master's channels before the
+    # Load RPC, so a rejected program still leaves a reset network
+    m = master()
+    m.handle("POST", "/run")
+    sess = m._sess = _FakeSession()
+    m.wire = _FakeWire()
+    r = m.handle("POST", "/load", body=program + b"&targetURI=misaka1", ctype=FORM)
+    assert r.code == code
+    assert sess.closed and m._sess is None and m.wire.resets == 1 and not m.is_running
+    # a stack target is rejected after the reset too
+    m._sess = sess2 = _FakeSession()
+    assert m.handle("POST", "/load", body=b"program=NOP&targetURI=misaka3", ctype=FORM).code == 400
+    assert sess2.closed and m.wire.resets == 2
+
+
+def test_default_is_stateful():
+    assert master().stateful  # the reference's semantics (program.go:80-92)
+
+
+def test_coalescer_routes_results_in_arrival_order():
+    seen = []
+    gate = threading.Event()
+
+    def run(vals):
+        gate.wait(5)
+        seen.append(list(vals))
+        return [(True, v * 10) for v in vals]
+
+    c = Coalescer(run)
+    out = {}
+
+    def client(i):
+        out[i] = c.submit(i)
+
+    ts = [threading.Thread(target=client, args=(i,)) for i in range(64)]
+    for t in ts:
+        t.start()
+        time.sleep(0.002)  # arrival order = i
+    gate.set()
+    for t in ts:
+        t.join(10)
+    assert out == {i: (True, 10 * i) for i in range(64)}
+    assert sum(map(len, seen)) == 64 and c.requests == 64
+    assert c.batches < 64  # requests that arrived during a launch shared the next one
+    flat = [v for b in seen for v in b]
+    assert flat == sorted(flat)  # each batch keeps arrival order, batches in order
+
+
+def test_coalescer_delivers_errors_to_the_batch():
+    c = Coalescer(lambda vals: 1 / 0)
+    with pytest.raises(ZeroDivisionError):
+        c.submit(1)
+    c2 = Coalescer(lambda vals: [(True, v) for v in vals], max_batch=3)
+    assert [c2.submit(i) for i in range(5)] == [(True, i) for i in range(5)]
 
 
 def test_boot_program_error_keeps_default_nop():
@@ -151,3 +229,56 @@ def test_stateful_master_keeps_node_state(gpu):
     e.handle("POST", "/run")
     assert [e.handle("POST", "/compute", body=f"value={x}".encode(), ctype=FORM).body for x in (5, 6)] == \
         ['{"value":7}\n', '{"value":8}\n']
+
+
+def _concurrent(port, path_vals, n_threads):
+    """n_threads clients released together; returns {i: (status, body)}."""
+    res = {}
+    bar = threading.Barrier(n_threads)
+
+    def client(i):
+        bar.wait(10)
+        st, _, body = post(port, "/compute", f"value={path_vals(i)}")
+        res[i] = (st, body)
+
+    ts = [threading.Thread(target=client, args=(i,)) for i in range(n_threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stateful", [True, False])
+def test_http_64_concurrent_clients(gpu, stateful):
+    m = MasterNode(NODE_INFO, PROGRAMS, stateful=stateful)
+    srv = make_server(m, port=0)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    try:
+        post(port, "/run")
+        res = _concurrent(port, lambda i: 1000 * i - 7, 64)
+        assert {i: r for i, r in res.items()} == {i: (200, f'{{"value":{1000 * i - 5}}}\n') for i in range(64)}
+        assert m.coalescer.requests == 64 and m.coalescer.batches <= 64
+    finally:
+        srv.shutdown()
+
+
+@pytest.mark.gpu
+def test_http_concurrent_stateful_running_sum(gpu):
+    # 64 concurrent /compute on one persistent instance: the calls are
+    # serialised (the reference's capacity-1 inChan/outChan), so the answers
+    # are exactly 10, 20, ..., 640 in some order
+    m = MasterNode({"acc": {"type": "program"}}, {"acc": "IN NIL\nADD 10\nOUT ACC"})
+    srv = make_server(m, port=0)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    try:
+        post(port, "/run")
+        res = _concurrent(port, lambda i: 0, 64)
+        vals = sorted(json.loads(b)["value"] for st, b in res.values())
+        assert vals == [10 * (k + 1) for k in range(64)]
+        assert m.coalescer.batches < 64  # bursts shared launches
+    finally:
+        srv.shutdown()
