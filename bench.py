@@ -37,6 +37,7 @@ METRIC = "simulated TIS node-instructions/sec (whole node) + /compute results/se
 SPEC_LANE_OPS = 256 * 4 * 32 * 2.4e9
 K_LANE_OPS = 4  # algorithmic lane-ops per retired node-instruction
 HBM_PEAK = 8.0e12
+L2_PEAK = 34.5e12  # aggregate XCD L2 bandwidth, MI355X_MICROARCH.md section L2
 
 WORKLOADS = {
     # name: (workload, network factory, lanes per GPU, generator kind, mask)
@@ -57,11 +58,39 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(nodes, gen_kind, mask, seconds=10.0):
-    """Oracle (the C port, test infrastructure) on the host cores, bounded sample."""
+def usable_cpus():
+    """(threads this process may run at once, whole-host CPU count, cgroup
+    quota in CPUs or None): the affinity mask bounded by the cgroup quota."""
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = host
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    for var in ("OMP_NUM_THREADS",):  # the box's CPU share, set by the harness
+        v = os.environ.get(var)
+        if v and v.isdigit() and quota is None:
+            quota = int(v)
+    return min(aff, quota or aff), host, quota
+
+
+def cpu_baseline(nodes, gen_kind, mask, seconds=10.0, refstruct_seconds=5.0):
+    """CPU baselines on the host cores, bounded samples of the same workload:
+    (i) the oracle (oracle/tis_oracle.c, the C port; test infrastructure)
+    batch-parallel on every usable core; (ii) the reference-structured
+    emulation (oracle/refstruct.py: a thread per node, a fresh loopback gRPC
+    call per network hop, program.go:80-92 / 475-566), sequential /compute
+    calls as the reference's single master serves them."""
     from oracle import pyoracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, host, quota = usable_cpus()
     on = pyoracle.OracleNet(nodes)
     n = 4096
     total_lanes = total_steps = 0
@@ -76,25 +105,56 @@ def cpu_baseline(nodes, gen_kind, mask, seconds=10.0):
         total_steps += int(sp.sum())
         if dt < seconds / 8:
             n *= 2
-    return {
+    rec = {
         "value": total_steps / t_total,
         "unit": "node-instr/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{total_lanes} lanes of the same workload in {t_total:.1f} s, oracle/tis_oracle.c, {threads} threads",
+        "sample": f"{total_lanes} lanes of the same workload in {t_total:.1f} s, oracle/tis_oracle.c, {threads} threads "
+                  f"(usable CPUs: affinity bounded by the cgroup / box CPU share)",
         "results_per_s": total_lanes / t_total,
+        "nproc": host,
+        "cpu_quota": quota,
     }
+    if refstruct_seconds > 0:
+        try:
+            from oracle import refstruct
+
+            xs = pyoracle.gen_inputs(SEED, 256, kind=gen_kind, mask=mask)
+            ref = on.compute_batch(xs)
+            xs = xs[(ref[1] & pyoracle.ST_HAS_OUTPUT) != 0]  # the reference's /compute hangs without an output
+            r = refstruct.time_compute(nodes, xs, seconds=refstruct_seconds) if xs.size else None
+            if r and r["results"]:
+                rec["reference_structured"] = {
+                    "value": r["node_instr_per_s"],
+                    "unit": "node-instr/s",
+                    "results_per_s": r["results_per_s"],
+                    "cores": r["threads"],
+                    "kind": "emulation",
+                    "sample": f"{r['results']} sequential /compute calls in {r['seconds']:.1f} s through "
+                              "oracle/refstruct.py: one thread per program node, a fresh insecure loopback gRPC "
+                              "channel per network hop (the reference dials per op over TLS), Python threads",
+                }
+            else:
+                rec["reference_structured"] = {"value": None, "note": "no /compute completed within the sample"}
+        except Exception as e:  # pragma: no cover - reported, never fatal
+            rec["reference_structured"] = {"value": None, "note": f"emulation failed: {e}"}
+    return rec
+
+
+def measured_profile(workload):
+    """The committed rocprofv3 PMC summary for this workload
+    (profiles/pmc_<workload>.json, tools/gpu_pmc_all.sh + tools/pmc_profile.py), or {}."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f)
 
 
 def measured_traffic(workload):
-    """HBM bytes per executor launch from the committed rocprofv3 PMC pass
-    for this workload (profiles/pmc_<workload>.json, written by
-    tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE), or None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+    """HBM bytes per executor launch from the committed PMC pass, or None."""
+    return measured_profile(workload).get("hbm_bytes_per_launch")
 
 
 def valu_peak(stream):
@@ -108,6 +168,63 @@ def valu_peak(stream):
     e1.record()
     torch.cuda.synchronize()
     return ops / (e0.elapsed_time(e1) * 1e-3)
+
+
+def http_leg(nodes, clients, seconds=5.0):
+    """Single-value /compute requests through the HTTP master (stateful, the
+    reference's semantics; concurrent requests coalesced into one launch per
+    burst): `clients` threads, each with a keep-alive connection, for about
+    `seconds`.  Python clients and server: this measures the drop-in surface,
+    not the executor."""
+    import http.client
+    import threading
+
+    from misaka_net_amd.master import MasterNode, make_server
+
+    info = {n.name: {"type": n.kind} for n in nodes if n.kind != "master"}
+    progs = {n.name: n.program for n in nodes if n.kind == "program"}
+    m = MasterNode(info, progs)
+    srv = make_server(m, port=0)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    hdr = {"Content-Type": "application/x-www-form-urlencoded"}
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+    c.request("POST", "/run", body="", headers=hdr)
+    c.getresponse().read()
+    counts = [0] * clients
+    errors = [0] * clients
+    stop = threading.Event()
+
+    def client(i):
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        k = 0
+        while not stop.is_set():
+            conn.request("POST", "/compute", body=f"value={i * 100003 + k}", headers=hdr)
+            r = conn.getresponse()
+            r.read()
+            if r.status == 200:
+                counts[i] += 1
+            else:
+                errors[i] += 1
+            k += 1
+        conn.close()
+
+    ts = [threading.Thread(target=client, args=(i,), daemon=True) for i in range(clients)]
+    b0, q0 = m.coalescer.batches, m.coalescer.requests
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    time.sleep(seconds)
+    stop.set()
+    for t in ts:
+        t.join(30)
+    dt = time.perf_counter() - t0
+    srv.shutdown()
+    batches, reqs = m.coalescer.batches - b0, m.coalescer.requests - q0
+    return {"requests_per_s": sum(counts) / dt, "clients": clients, "errors": sum(errors),
+            "launches": batches, "requests_per_launch": reqs / max(1, batches),
+            "mode": "stateful (one persistent network instance, mk_session_compute_seq per burst)",
+            "note": "Python ThreadingHTTPServer + Python clients in one process; not the value"}
 
 
 def main():
@@ -132,6 +249,13 @@ def main():
     ap.add_argument("--host-io", action="store_true",
                     help="also time mk_compute_batch on host buffers (int64 in, int32 out + u8 status over PCIe); "
                          "reported as host_io, never as value")
+    ap.add_argument("--http", type=int, default=0, metavar="CLIENTS",
+                    help="also time single-value /compute requests through the HTTP master with this many "
+                         "concurrent keep-alive clients (reported as http, never as value)")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="N > 1: rank 0 checks the gathered outputs against one launch over every global lane")
+    ap.add_argument("--refstruct-seconds", type=float, default=5.0,
+                    help="sample length of the reference-structured CPU emulation (0: skip)")
     args = ap.parse_args()
     if args.interp:
         args.mode = "interp"
@@ -240,6 +364,14 @@ def main():
     torch.cuda.synchronize()
     launch_s = k0.elapsed_time(k1) * 1e-3 / args.steps
 
+    peak_meas = None
+    if rank == 0:
+        try:
+            peak_meas = valu_peak(sh)
+        except Exception as e:  # pragma: no cover
+            log("valu probe failed:", e)
+    peak = max(SPEC_LANE_OPS, peak_meas or 0.0)
+
     # per-rank -> whole job (max time over ranks, summed work)
     t = torch.tensor([wall, kernel_s, launch_s], dtype=torch.float64, device="cuda")
     tot = mk.dist.reduce_counters(stats.clone(), dist)
@@ -250,15 +382,38 @@ def main():
     retired, with_out, finished = int(tot[0]), int(tot[1]), int(tot[2])
     assert finished == lanes * world * args.steps, (finished, lanes, world, args.steps)
 
-    gather_ms = None
-    if args.gather and dist:
+    # End to end (N > 1): K steps of launch + ordered gather of the step's
+    # int32 outputs and status bytes to rank 0 (RCCL over xGMI, SURVEY.md
+    # section 8 row e), timed like the compute-only loop.  Reported beside
+    # `value`, which stays the sharded compute (no data-path collective).
+    e2e = None
+    if dist and (world > 1 or args.gather):
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        mk.dist.gather_outputs(out, dist)
-        mk.dist.gather_outputs(st, dist)
+        for _ in range(args.steps):
+            step(False)
+            g_out = mk.dist.gather_outputs(out, dist)
+            g_st = mk.dist.gather_outputs(st, dist)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+        tt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        e2e_s = tt.item()
+        e2e = {"value": None, "ms_per_step": e2e_s / args.steps * 1e3,
+               "gathered_bytes_per_step": 5 * lanes * world, "collective": "ordered gather to rank 0 "
+               f"({dist.get_backend()}), outputs int32 + status u8"}
+        if args.verify_gather and rank == 0:
+            # the gathered shards == one launch over all world x lanes global lanes
+            xf = torch.empty(lanes * world, dtype=torch.int32, device="cuda")
+            mk.generate_inputs_device(lanes * world, xf.data_ptr(), seed=SEED, gen_kind=gen_kind, gen_mask=mask,
+                                      offset=0, device=dev, stream=sh)
+            of = torch.empty_like(xf)
+            sf = torch.empty(lanes * world, dtype=torch.uint8, device="cuda")
+            net.compute_device(lanes * world, out_ptr=of.data_ptr(), status_ptr=sf.data_ptr(), in_ptr=xf.data_ptr(),
+                               device=dev, stream=sh, mode=args.mode)
+            torch.cuda.synchronize()
+            e2e["verified"] = bool(torch.equal(of, g_out) and torch.equal(sf, g_st))
+            assert e2e["verified"], "gathered outputs differ from a single launch over the global lanes"
 
     host_io = None
     if args.host_io and rank == 0:
@@ -280,59 +435,88 @@ def main():
         }
 
     value = retired / wall_max
-    per_gpu_kernel_rate = retired / world / kern_max
-    peak_meas = None
-    if rank == 0:
-        try:
-            peak_meas = valu_peak(sh)
-        except Exception as e:  # pragma: no cover
-            log("valu probe failed:", e)
-    peak = max(SPEC_LANE_OPS, peak_meas or 0.0)
-    # per launch of the executor kernel: algorithmic lane-ops and bytes
+    if e2e is not None:
+        e2e["value"] = retired / (e2e["ms_per_step"] * 1e-3 * args.steps)
+        e2e["results_per_s"] = with_out / (e2e["ms_per_step"] * 1e-3 * args.steps)
+    # ---- roofline of the dominant kernel, per launch -----------------------
     instr_per_launch = retired / world / args.steps
-    achieved = K_LANE_OPS * instr_per_launch / launch_max
+    prof = measured_profile(name) if not args.mode and not args.gen_inputs else {}
+    if prof and abs(prof.get("retired_per_launch", 0) - instr_per_launch) > 0.01 * instr_per_launch:
+        prof = {}  # counters of another lane count / network: not this launch
+    traffic = prof.get("hbm_bytes_per_launch")
     # int32 input read, int32 out + u8 status written, stack slots written and read back
-    bytes_per_lane = (0 if args.gen_inputs else 4) + 4 + 1 + 4 * STACK_OPS_PER_LANE.get(args.config, 0)
-    bytes_per_launch = bytes_per_lane * lanes
+    io_bytes = ((0 if args.gen_inputs else 4) + 4 + 1) * lanes
+    slot_bytes = 4 * STACK_OPS_PER_LANE.get(args.config, 0) * lanes
+    bytes_per_launch = io_bytes + slot_bytes
     hbm_achieved = bytes_per_launch / launch_max
-    traffic = measured_traffic(name)
+    # Lower bound on the launch's memory time: the bytes PMC saw leave the
+    # XCDs' L2s at the HBM peak, the algorithmic bytes that never did
+    # (stack slots popped back while still in L2) at the L2 peak.
+    fabric = min(traffic, bytes_per_launch) if traffic else bytes_per_launch
+    t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / L2_PEAK
     hbm = {
         "bound": "hbm",
         "achieved": hbm_achieved / 1e9,
-        "peak": HBM_PEAK / 1e9,
+        "peak": bytes_per_launch / t_mem / 1e9,
         "unit": "GB/s",
-        "frac": hbm_achieved / HBM_PEAK,
+        "frac": t_mem / launch_max,
         "traffic": traffic,
-        "bytes_per_lane": bytes_per_lane,
+        "bytes_per_lane": bytes_per_launch // lanes,
         "bytes_per_launch": bytes_per_launch,
         "launch_us": launch_max * 1e6,
+        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
+                  if traffic and bytes_per_launch > fabric * 1.001 else "peak = HBM 8 TB/s"),
+        "counter_source": prof.get("source"),
     }
-    issue = {
-        "bound": "valu",
-        "achieved": achieved / 1e12,
-        "peak": peak / 1e12,
-        "unit": "Tlane-op/s",
-        "frac": achieved / peak,
-        "traffic": traffic,
-        "k_lane_ops_per_instr": K_LANE_OPS,
-        "peak_spec": SPEC_LANE_OPS / 1e12,
-        "peak_measured": None if peak_meas is None else peak_meas / 1e12,
-        "launch_us": launch_max * 1e6,
-    }
-    if hbm["frac"] > 1.0:
-        hbm["note"] = ("algorithmic bytes above the HBM peak: stack slots written and popped back while still in "
-                       "L2/MALL; `traffic` (PMC) is what reached HBM")
-    if issue["frac"] > 1.0:
-        issue["note"] = ("k = 4 lane-ops per node-instruction is the frozen model; the schedule compiler turns "
-                         "port hand-offs, SWP/SAV and loop control into register renames, so fewer are issued")
+    sq = prof.get("sq", {})
+    if sq.get("SQ_INSTS_VALU"):
+        # executed work from the committed SQ counters: VALU wave-instructions x 64 lanes
+        exec_ops = sq["SQ_INSTS_VALU"] * 64
+        issue = {
+            "bound": "valu",
+            "achieved": exec_ops / launch_max / 1e12,
+            "peak": peak / 1e12,
+            "unit": "Tlane-op/s",
+            "frac": exec_ops / launch_max / peak,
+            "traffic": traffic,
+            "model": "executed VALU lane-ops per launch (PMC SQ_INSTS_VALU x 64) / launch time",
+            "valu_lane_ops_per_instr": prof.get("valu_lane_ops_per_instr"),
+            "salu_per_instr": prof.get("salu_per_instr"),
+            "valu_lane_util_norm": prof.get("valu_lane_util_norm"),
+            "k_model_frac": K_LANE_OPS * instr_per_launch / launch_max / peak,
+            "peak_spec": SPEC_LANE_OPS / 1e12,
+            "peak_measured": None if peak_meas is None else peak_meas / 1e12,
+            "launch_us": launch_max * 1e6,
+            "counter_source": prof.get("source"),
+        }
+    else:
+        achieved = K_LANE_OPS * instr_per_launch / launch_max
+        issue = {
+            "bound": "valu",
+            "achieved": achieved / 1e12,
+            "peak": peak / 1e12,
+            "unit": "Tlane-op/s",
+            "frac": achieved / peak,
+            "traffic": traffic,
+            "model": "k = 4 lane-ops per retired node-instruction (BASELINE.md section 2; no PMC profile for "
+                     "this launch)",
+            "k_lane_ops_per_instr": K_LANE_OPS,
+            "peak_spec": SPEC_LANE_OPS / 1e12,
+            "peak_measured": None if peak_meas is None else peak_meas / 1e12,
+            "launch_us": launch_max * 1e6,
+        }
     # The dominant kernel's roofline is the tighter of the two bounds: the
     # byte stream for short networks (C2, C3), integer issue for long ones.
-    hbm_bound = hbm_achieved / HBM_PEAK >= achieved / peak
+    hbm_bound = hbm["frac"] >= issue["frac"]
+
+    http = None
+    if args.http and rank == 0:
+        http = http_leg(nodes, args.http, seconds=5.0)
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the host-core baseline is an N=1 figure
-            cpu = cpu_baseline(nodes, gen_kind, mask, args.cpu_seconds)
+            cpu = cpu_baseline(nodes, gen_kind, mask, args.cpu_seconds, args.refstruct_seconds)
         rec = {
             "metric": METRIC,
             "value": value,
@@ -364,10 +548,12 @@ def main():
             "roofline_hbm": hbm,
             "cpu_baseline": cpu,
         }
-        if gather_ms is not None:
-            rec["gather_ms"] = gather_ms
+        if e2e is not None:
+            rec["end_to_end"] = e2e
         if host_io is not None:
             rec["host_io"] = host_io
+        if http is not None:
+            rec["http"] = http
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -32,6 +32,9 @@ def gather_outputs(out, dist, dst: int = 0):
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return out
     world, rank = dist.get_world_size(), dist.get_rank()
+    if out.is_cuda and dist.get_backend() == "gloo":  # gloo gathers host tensors only
+        g = gather_outputs(out.cpu(), dist, dst)
+        return None if g is None else g.to(out.device)
     if rank == dst:
         buf = torch.empty(world * out.numel(), dtype=out.dtype, device=out.device)
         dist.gather(out, gather_list=list(buf.view(world, -1).unbind(0)), dst=dst)
