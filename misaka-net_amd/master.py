@@ -395,4 +395,10 @@ def make_server(master: MasterNode, host: str = "127.0.0.1", port: int = 8000) -
         def log_message(self, *a):
             pass
 
-    return ThreadingHTTPServer((host, port), Handler)
+    class Server(ThreadingHTTPServer):
+        # net/http accepts without a fixed backlog; socketserver's default of 5
+        # resets bursts of concurrent clients
+        request_queue_size = 1024
+        daemon_threads = True
+
+    return Server((host, port), Handler)

@@ -282,3 +282,20 @@ def test_http_concurrent_stateful_running_sum(gpu):
         assert m.coalescer.batches < 64  # bursts shared launches
     finally:
         srv.shutdown()
+
+
+def test_http_server_takes_bursts_of_clients():
+    # 64 clients connecting at once (the listen backlog must hold them; the
+    # executor is replaced by a fake so this runs without a GPU)
+    m = master()
+    m.coalescer._run = lambda vals: [(True, v + 2) for v in vals]
+    srv = make_server(m, port=0)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    try:
+        post(port, "/run")
+        res = _concurrent(port, lambda i: i, 64)
+        assert res == {i: (200, f'{{"value":{i + 2}}}\n') for i in range(64)}
+        assert m.coalescer.requests == 64
+    finally:
+        srv.shutdown()
