@@ -1098,6 +1098,7 @@ struct JitState {
     JitShape shape = JIT_STREAM;
     uint64_t max_steps = UINT64_MAX; // stream shape: launches need budget > max_steps
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
+    uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
 };
@@ -1492,16 +1493,16 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     }
     const auto t0 = std::chrono::steady_clock::now();
     std::string lane;
-    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy)) return false;
+    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
-    J.block = J.heavy ? kJitHeavyBlock : kJitBlock;
+    J.block = J.heavy ? kJitHeavyBlock : J.pool ? kJitPoolBlock : kJitBlock;
     if (lane.size() > lim.max_src_bytes) {
         J.why = "lane source of " + std::to_string(lane.size()) + " B exceeds the native tier's compile bound (" +
                 std::to_string(lim.max_src_bytes) + " B)";
         return false;
     }
     auto job = std::make_shared<HiprtcJob>();
-    job->src = jit_module_source(lane, J.shape, J.heavy, lim);
+    job->src = jit_module_source(lane, J.shape, J.heavy, lim, J.pool);
     J.src_bytes = job->src.size();
     std::thread(hiprtc_run, job).detach();
     {
@@ -1571,8 +1572,10 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
         blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
         lanes = (uint64_t)blocks * block;
     }
+    // stack-slot columns: one per thread, or (pool kernel) one per pool slot
+    const uint64_t slot_cols = sc->jit.pool ? (uint64_t)blocks * sc->jit.pool : lanes;
     if (P.nslots) {
-        const size_t need = (size_t)P.nslots * lanes * sizeof(int32_t);
+        const size_t need = (size_t)P.nslots * slot_cols * sizeof(int32_t);
         if (need > sd.slots_bytes) {
             if (sd.d_slots) {
                 (void)hipDeviceSynchronize();
@@ -1601,7 +1604,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
     p.part_rows = (uint32_t)(c.partials_bytes / 64);
     p.slots = P.nslots ? sd.d_slots : nullptr;
-    p.lanes = lanes;
+    p.lanes = slot_cols;
     p.vlanes = lanes;
     const uintptr_t va = 4u * kJitStreamLanes;
     p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
@@ -2160,10 +2163,10 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     std::string s;
     if (t == mk::TIER_NATIVE) {
         char tail[160];
-        snprintf(tail, sizeof tail, " shape=%s source=%zuB code=%zuB compile=%.2fs",
+        snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs",
                  sc->jit.shape == mk::JIT_MACHINE ? "machine" : sc->jit.heavy ? "stream-heavy" : "stream",
-                 sc->jit.src_bytes, sc->jit.code.size(),
-                 sc->jit.compile_s);
+                 sc->jit.pool ? ("-pool" + std::to_string(sc->jit.pool)).c_str() : "", sc->jit.src_bytes,
+                 sc->jit.code.size(), sc->jit.compile_s);
         s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
     } else {
         const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
@@ -2207,9 +2210,10 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     else {
         mk::JitShape shape;
         bool heavy = false;
-        if (mk::jit_lane_source(sc->prog, h->jit_lim, lane, why, &shape, nullptr, &heavy))
+        uint32_t pool = 0;
+        if (mk::jit_lane_source(sc->prog, h->jit_lim, lane, why, &shape, nullptr, &heavy, false, &pool))
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
-                                                                    h->jit_lim));
+                                                                    h->jit_lim, pool));
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

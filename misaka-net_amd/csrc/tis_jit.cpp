@@ -1130,6 +1130,38 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    L.st = 0u;");
     e.line("    L.outv = 0;");
     e.line("}");
+    // The pool kernel's parked lanes (kMachinePoolKernel): a lane between
+    // superblocks is its registers, superblock and step count (out / status
+    // are set only on the way to MK_SB_DONE, when the lane is retired, never
+    // parked), plus the input index it answers.  Struct of arrays in LDS.
+    e.line("#define MK_NV %zuu", nv);
+    e.line("#ifdef MK_POOL");
+    e.line("struct MkPool {");
+    for (uint32_t r = 0; r < p.nregs; ++r)
+        if (g.used_reg[r]) e.line("    int64_t r%u[MK_POOL];", r);
+    e.line("    uint64_t idx[MK_POOL];");
+    e.line("    uint32_t sb[MK_POOL];");
+    e.line("    uint32_t steps[MK_POOL];");
+    e.line("};");
+    e.line("MK_FN void mk_park(MkPool &P, const uint32_t s, const MkLane &L, const uint64_t idx)");
+    e.line("{");
+    for (uint32_t r = 0; r < p.nregs; ++r)
+        if (g.used_reg[r]) e.line("    P.r%u[s] = L.r%u;", r, r);
+    e.line("    P.idx[s] = idx;");
+    e.line("    P.steps[s] = L.steps;");
+    e.line("    P.sb[s] = L.sb;");
+    e.line("}");
+    e.line("MK_FN void mk_unpark(const MkPool &P, const uint32_t s, MkLane &L, uint64_t &idx)");
+    e.line("{");
+    for (uint32_t r = 0; r < p.nregs; ++r)
+        if (g.used_reg[r]) e.line("    L.r%u = P.r%u[s];", r, r);
+    e.line("    idx = P.idx[s];");
+    e.line("    L.steps = P.steps[s];");
+    e.line("    L.sb = P.sb[s];");
+    e.line("    L.st = 0u;");
+    e.line("    L.outv = 0;");
+    e.line("}");
+    e.line("#endif");
     // mk_run(u, ...): superblock variant u for a lane sitting on it (L.sb == u).
     // MK_LOOP_NEED() / MK_KEEP(m, need) come from the includer: the wave's
     // policy for leaving a loop early so that finished lanes can refill.
@@ -1254,12 +1286,23 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 } // namespace
 
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
-                     uint64_t *max_steps, bool *heavy, bool checked)
+                     uint64_t *max_steps, bool *heavy, bool checked, uint32_t *pool)
 {
     Graph g;
     if (!analyze(p, lim, g, why)) return false;
     Emitter e;
     const JitShape s = lim.force_stream ? JIT_STREAM : (lim.force_machine || g.cyclic) ? JIT_MACHINE : JIT_STREAM;
+    if (pool) {
+        // lane pool of the machine shape: slots per wave from the parked state size
+        size_t used = 0;
+        for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1 : 0;
+        const size_t bytes = 8 * used + 16;
+        uint32_t m = lim.pool ? lim.pool : (uint32_t)std::min<size_t>(kJitPoolMaxSlots, kJitPoolBytes / bytes / 64 * 64);
+        m = m / 64 * 64;
+        const bool ok = s == JIT_MACHINE && lim.compact && g.entry.size() <= kJitPoolMaxVariants &&
+                        m >= (lim.pool ? 64u : kJitPoolMinSlots) && m <= 4096 && bytes * m <= 65536;
+        *pool = ok ? m : 0;
+    }
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else
@@ -1471,21 +1514,197 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_SLOT_NT", l.slot_nt);
     flag("MK_JIT_IO_NT", l.io_nt);
     flag("MK_JIT_COMPACT", l.compact);
+    num("MK_JIT_POOL", l.pool);
     return l;
 }
 
 std::string JitLimits::key() const
 {
     char b[256];
-    snprintf(b, sizeof b, "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,compact=%d",
+    snprintf(b, sizeof b,
+             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,compact=%d,pool=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
-             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, (int)compact);
+             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, (int)compact, pool);
     return b;
 }
 
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim)
+// Kernel of the machine shape with lane compaction.  One wave per block,
+// owning a pool of MK_POOL parked lanes in LDS (MkPool: registers,
+// superblock, steps, input index) and a histogram of how many parked lanes
+// sit on each superblock variant.  Each turn:
+//   1. free slots take new inputs, 64 at a time (chunks of 64 inputs dealt
+//      round-robin over the waves);
+//   2. the variant u with the most parked lanes is chosen, and up to 64 of
+//      its lanes are claimed into registers (MkLane, one per thread);
+//   3. mk_run(u) runs them together.  A lane that left u is parked again on
+//      its new variant, or, at MK_SB_DONE, answers its input and frees its
+//      slot.  For a self-loop (mk_is_loop) the loop leaves once a quarter of
+//      its lanes have left (MK_LOOP_NEED), and the group is topped up from
+//      the lanes parked on u and run again -- as long as it is no smaller
+//      than the largest group parked elsewhere; otherwise its lanes are
+//      parked (still on u, at an iteration boundary) and the turn ends.
+// So the lanes of a data-dependent loop stay together whatever their trip
+// counts: a lane that leaves is replaced by one waiting at the loop head,
+// instead of idling (predicated) until the group's longest trip ends.
+// Stack slots belong to pool slots (column wave * MK_POOL + slot, stride
+// p.lanes = waves * MK_POOL), so a lane's stacks follow it between threads.
+static const char *const kMachinePoolKernel = R"(
+#define MK_SLOT_FREE 0xFFFFFFFFu
+#define MK_SLOT_BUSY 0xFFFFFFFDu
+#define MK_NONE 0xFFFFFFFFu
+MK_FN uint32_t mk_rank(unsigned long long b)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+MK_FN void mk_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// Whole wave: each lane with `want` gets a distinct pool slot whose sb is
+// `key` (the lane of rank r among the wanting lanes the r-th such slot), or
+// MK_NONE when there are fewer such slots; *got = slots handed out.
+MK_FN uint32_t mk_claim(const uint32_t *sb, uint32_t *xfer, uint32_t key, bool want, uint32_t &got)
+{
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long wb = __ballot(want);
+    const uint32_t nwant = (uint32_t)__popcll(wb);
+    uint32_t found = 0u;
+    for (uint32_t base = 0u; base < MK_POOL && found < nwant; base += 64u) {
+        const uint32_t s = base + lane;
+        const bool m = sb[s] == key;
+        const unsigned long long mb = __ballot(m);
+        const uint32_t k = found + mk_rank(mb);
+        if (m && k < nwant) xfer[k] = s;
+        found += (uint32_t)__popcll(mb);
+    }
+    mk_wave_sync();
+    got = found < nwant ? found : nwant;
+    const uint32_t r = mk_rank(wb);
+    const uint32_t s = want && r < got ? xfer[r] : MK_NONE;
+    mk_wave_sync();
+    return s;
+}
+// Whole wave: (count << 16 | (0xFFFF - v)) of the variant with the most parked lanes.
+MK_FN uint32_t mk_pick(const uint32_t *hist)
+{
+    uint32_t best = 0u;
+    for (uint32_t v = threadIdx.x; v < MK_NV; v += 64u) {
+        const uint32_t c = hist[v];
+        const uint32_t key = c ? (c << 16) | (0xFFFFu - v) : 0u;
+        best = key > best ? key : best;
+    }
+    return MK_WAVE_MAX(best);
+}
+
+extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
+{
+    __shared__ MkPool P;
+    __shared__ uint32_t hist[MK_NV];
+    __shared__ uint32_t xfer[64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t gw = blockIdx.x, nw = gridDim.x;
+    const uint64_t gid = gw * 64u + lane;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t s = lane; s < MK_POOL; s += 64u) P.sb[s] = MK_SLOT_FREE;
+    for (uint32_t v = lane; v < MK_NV; v += 64u) hist[v] = 0u;
+    mk_wave_sync();
+    uint32_t nfree = MK_POOL;
+    uint64_t chunk = gw; // next 64 inputs: [chunk * 64, chunk * 64 + 64)
+    int32_t *const sbase = p.slots ? p.slots + gw * (uint64_t)MK_POOL : (int32_t *)0;
+    MkLane L;
+    mk_init(L, 0);
+    uint32_t my = MK_NONE; // pool slot of the lane this thread holds
+    uint64_t myidx = 0;
+    // retire a held lane that left u: answer its input or park it
+    auto leave = [&](const uint32_t u, const bool all) -> uint32_t {
+        const bool go = my != MK_NONE && (all || L.sb != u);
+        const bool done = go && L.sb == MK_SB_DONE;
+        if (done) {
+            p.out[myidx] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+            p.status[myidx] = (uint8_t)L.st;
+            if (p.steps) p.steps[myidx] = L.steps;
+            count_lane(cnt, L.steps, L.st);
+            P.sb[my] = MK_SLOT_FREE;
+        } else if (go) {
+            mk_park(P, my, L, myidx);
+            atomicAdd(&hist[L.sb], 1u);
+        }
+        if (go) my = MK_NONE;
+        mk_wave_sync();
+        return (uint32_t)__popcll(__ballot(done));
+    };
+    // new inputs into free slots, 64 at a time
+    auto fill = [&]() {
+        while (nfree >= 64u && chunk * 64u < p.n) {
+            const uint64_t i = chunk * 64u + lane;
+            const bool has = i < p.n;
+            uint32_t got;
+            const uint32_t s = mk_claim(P.sb, xfer, MK_SLOT_FREE, has, got);
+            if (s != MK_NONE) {
+                MkLane F;
+                mk_init(F, sched_input(p, i));
+                mk_park(P, s, F, i);
+            }
+            if (lane == 0u) hist[0] += got;
+            mk_wave_sync();
+            nfree -= got;
+            chunk += nw;
+        }
+    };
+    for (;;) {
+        fill();
+        const uint32_t best = mk_pick(hist);
+        if (!(best >> 16)) break; // nothing parked, no inputs left
+        const uint32_t u = 0xFFFFu - (best & 0xFFFFu);
+        uint32_t got;
+        my = mk_claim(P.sb, xfer, u, true, got);
+        if (!got) break; // histogram and pool disagree: stop rather than spin (lanes stay unanswered)
+        if (my != MK_NONE) {
+            mk_unpark(P, my, L, myidx);
+            P.sb[my] = MK_SLOT_BUSY;
+        }
+        if (lane == 0u) hist[u] -= got;
+        mk_wave_sync();
+        const bool loop = mk_is_loop(u);
+        for (;;) {
+            // loop variants: the group's largest step count (exec is full here)
+            const uint32_t smax = loop ? MK_WAVE_MAX(my != MK_NONE ? L.steps : 0u) : 0u;
+            const uint32_t pol = loop ? (12u << 8) | (1u << 16) : 0u; // leave a loop at a quarter gone
+            if (my != MK_NONE) mk_run(u, L, p.budget, sbase ? sbase + my : (int32_t *)0, p.lanes, pol, smax);
+            if (!loop) {
+                nfree += leave(u, true);
+                break;
+            }
+            nfree += leave(u, false);
+            fill();
+            // top the group up from the lanes parked on u
+            uint32_t add;
+            const uint32_t s = mk_claim(P.sb, xfer, u, my == MK_NONE, add);
+            if (s != MK_NONE) {
+                my = s;
+                mk_unpark(P, my, L, myidx);
+                P.sb[my] = MK_SLOT_BUSY;
+            }
+            if (lane == 0u) hist[u] -= add;
+            mk_wave_sync();
+            const uint32_t nin = (uint32_t)__popcll(__ballot(my != MK_NONE));
+            if (!nin) break;
+            if (nin < (mk_pick(hist) >> 16)) { // a larger group waits elsewhere
+                nfree += leave(u, true);
+                break;
+            }
+        }
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+)";
+
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
+                              uint32_t pool)
 {
     Emitter e;
+    if (shape == JIT_MACHINE && pool) e.line("#define MK_POOL %uu", pool);
     // hiprtc declares the fixed-width integer types in __hip_internal only
     e.line("typedef __hip_internal::int8_t int8_t;");
     e.line("typedef __hip_internal::uint8_t uint8_t;");
@@ -1559,7 +1778,9 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.s += kDeviceCommon;
     e.s += "\n";
     e.s += lane_src;
-    e.s += shape == JIT_MACHINE ? kMachineKernel : heavy ? kStreamKernelHeavy : kStreamKernel;
+    e.s += shape == JIT_MACHINE ? (pool ? kMachinePoolKernel : kMachineKernel)
+           : heavy                ? kStreamKernelHeavy
+                                  : kStreamKernel;
     return e.s;
 }
 

@@ -69,8 +69,13 @@ struct JitLimits {
     size_t prefetch = kJitPrefetchLoads;   // MK_JIT_PREFETCH (0: off)
     size_t heavy_ops = kJitHeavyOps;       // MK_JIT_HEAVY_OPS
     uint64_t slot_bytes = kJitSlotBytes;   // MK_JIT_SLOT_BYTES
-    // Compaction of divergent self-loops in the machine shape (MK_JIT_COMPACT=0 off).
+    // Lane compaction in the machine shape (kMachinePoolKernel): each wave
+    // parks lanes between superblocks in an LDS pool and runs full groups of
+    // lanes that sit on the same superblock.  MK_JIT_COMPACT=0: the pool-less
+    // kernel (generations); MK_JIT_POOL=<slots per wave, multiple of 64>
+    // overrides the size (0: from the lane state size, kJitPoolBytes).
     bool compact = true;
+    uint32_t pool = 0;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
@@ -93,21 +98,28 @@ struct JitLimits {
 // runs one lane per thread in 64-thread blocks instead of 4-lane tiles).
 // The checked lane (mk_lane of the stream shape) is emitted only with
 // `checked` (host tests); the GPU module does not compile it.
+// pool: slots per wave of the machine shape's lane pool (0: pool-less kernel).
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why,
                      JitShape *shape = nullptr, uint64_t *max_steps = nullptr, bool *heavy = nullptr,
-                     bool checked = false);
+                     bool checked = false, uint32_t *pool = nullptr);
 
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of
 // the given shape.
 // lim.policy (the machine shape's policy word) is compiled in.
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim);
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
+                              uint32_t pool = 0);
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
 constexpr int kJitHeavyBlock = 64;
+constexpr int kJitPoolBlock = 64;         // the pool kernel: one wave per block, its own pool
+constexpr size_t kJitPoolBytes = 12288;   // LDS for one wave's lane pool (slots = bytes / lane state)
+constexpr uint32_t kJitPoolMaxSlots = 256;
+constexpr uint32_t kJitPoolMinSlots = 128;
+constexpr size_t kJitPoolMaxVariants = 1024; // LDS histogram of parked lanes per superblock variant
 // Heavy-kernel slot layout: up to this many slots per lane, wave-blocked
 // ([wave][slot][64 lanes]: a wave's stacks are one contiguous block, read
 // and written by buffer ops whose slot offset s * 256 is a scalar, which

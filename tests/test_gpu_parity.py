@@ -89,11 +89,15 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
 # loops), once on the default path and once with the machine shape and a
 # policy that leaves loops early (so groups re-enter loops with smaller
 # and mixed step counts).
-@pytest.mark.parametrize("variant", ["auto", "machine-early-exit"])
+@pytest.mark.parametrize("variant", ["auto", "machine-early-exit", "pool64"])
 def test_loop_phases_bit_exact(gpu, monkeypatch, variant):
-    if variant != "auto":
+    if variant == "machine-early-exit":  # the pool-less kernel, leaving loops early
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+        monkeypatch.setenv("MK_JIT_COMPACT", "0")
         monkeypatch.setenv("MK_JIT_POLICY", "8,12,16")
+    if variant == "pool64":  # the smallest lane pool: groups refill from few parked lanes
+        monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+        monkeypatch.setenv("MK_JIT_POOL", "64")
     for label, nodes, xs, kw in loop_cases(n=4096):
         xs = np.asarray(xs, np.int64)
         assert_same(mk.Network(nodes).compute_batch(xs, **kw), oracle(nodes, xs, **kw), f"{label} {variant}")
@@ -416,13 +420,20 @@ def test_wide_immediates_on_symbolic_acc(gpu, mode):
 
 
 # The native tier's two kernel shapes (tis_jit.h): acyclic schedules stream,
-# cyclic ones run as per-lane state machines with refill.  Force the machine
-# shape on every network (MK_JIT_SHAPE is read when a network's kernel is
-# generated) and vary its wave policy (MK_JIT_POLICY, compiled into each new network's kernel).
-@pytest.mark.parametrize("policy", ["8,12,16", "1,0,64", "64,16,1", "16,8,4"])
+# cyclic ones run as per-lane state machines.  Force the machine shape on
+# every network (the knobs are read when a network is loaded) and run both of
+# its kernels: the lane-pool kernel (compaction; default, and with pools of
+# 64 / 128 slots) and the pool-less one under several wave policies
+# (MK_JIT_POLICY, compiled into each new network's kernel).
+@pytest.mark.parametrize("policy", ["pool", "pool64", "pool128", "8,12,16", "1,0,64", "64,16,1", "16,8,4"])
 def test_machine_shape_and_policies(gpu, monkeypatch, policy):
     monkeypatch.setenv("MK_JIT_SHAPE", "machine")
-    monkeypatch.setenv("MK_JIT_POLICY", policy)
+    if policy.startswith("pool"):
+        if policy != "pool":
+            monkeypatch.setenv("MK_JIT_POOL", policy[4:])
+    else:
+        monkeypatch.setenv("MK_JIT_COMPACT", "0")
+        monkeypatch.setenv("MK_JIT_POLICY", policy)
     cases = [("c2", mk.networks.example_network(), po.gen_inputs(SEED, 5000), {}),
              ("c3", mk.networks.sample_network(), po.gen_inputs(SEED, 5000), {}),
              ("c5", mk.networks.countdown_network(), po.gen_inputs(SEED, 5000, kind=1, mask=1023), {}),
@@ -437,6 +448,7 @@ def test_machine_shape_and_policies(gpu, monkeypatch, policy):
         plan = net.plan(stack_cap=kw.get("stack_cap"), stop_on_output=kw.get("stop_on_output", False))
         if label.startswith("c"):
             assert "shape=machine" in plan, plan
+            assert ("-pool" in plan) == policy.startswith("pool"), plan
         assert_same(got, oracle(nodes, xs, **kw), f"{label} policy {policy}")
 
 

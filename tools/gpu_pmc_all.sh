@@ -14,7 +14,7 @@ SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VA
 for cfg in "$@"; do
   for pass in FETCH_SIZE WRITE_SIZE SQ; do
     if [ $pass = SQ ]; then ctr=$SQ; else ctr=$pass; fi
-    echo "[pmc] $(date +%T) $cfg $pass"
+    echo "[pmc] $(date +%T) $cfg $pass"; mkdir -p "$OUT/$cfg"
     timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$OUT/$cfg/$pass" -o p -- \
       python3 bench.py --config $cfg --steps 6 --warmup 1 --no-cpu-baseline > "$OUT/$cfg/$pass.log" 2>&1 \
       || { echo "[pmc] failed $cfg $pass"; tail -5 "$OUT/$cfg/$pass.log"; exit 1; }
