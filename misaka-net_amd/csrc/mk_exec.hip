@@ -1495,12 +1495,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     std::string lane;
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
-    J.block = J.heavy ? kJitHeavyBlock : J.pool ? kJitPoolBlock : kJitBlock;
-    if (lane.size() > lim.max_src_bytes) {
-        J.why = "lane source of " + std::to_string(lane.size()) + " B exceeds the native tier's compile bound (" +
-                std::to_string(lim.max_src_bytes) + " B)";
-        return false;
-    }
+    J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, lim, J.pool);
     J.src_bytes = job->src.size();
@@ -1573,7 +1568,9 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
         lanes = (uint64_t)blocks * block;
     }
     // stack-slot columns: one per thread, or (pool kernel) one per pool slot
-    const uint64_t slot_cols = sc->jit.pool ? (uint64_t)blocks * sc->jit.pool : lanes;
+    const uint64_t slot_cols = sc->jit.pool >= 64 ? (uint64_t)blocks * sc->jit.pool
+                               : sc->jit.pool      ? lanes * sc->jit.pool
+                                                   : lanes;
     if (P.nslots) {
         const size_t need = (size_t)P.nslots * slot_cols * sizeof(int32_t);
         if (need > sd.slots_bytes) {
@@ -2165,7 +2162,10 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         char tail[160];
         snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs",
                  sc->jit.shape == mk::JIT_MACHINE ? "machine" : sc->jit.heavy ? "stream-heavy" : "stream",
-                 sc->jit.pool ? ("-pool" + std::to_string(sc->jit.pool)).c_str() : "", sc->jit.src_bytes,
+                 sc->jit.pool >= 64 ? ("-pool" + std::to_string(sc->jit.pool)).c_str()
+                 : sc->jit.pool     ? ("-k" + std::to_string(sc->jit.pool)).c_str()
+                                    : "",
+                 sc->jit.src_bytes,
                  sc->jit.code.size(), sc->jit.compile_s);
         s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
     } else {

@@ -3,6 +3,7 @@
 // (lib/libmisaka_amd_check.so) so the schedule compiler can be fuzzed against
 // the CPU oracle without a GPU.  It is not part of the product library and
 // no product entry point can reach it.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -169,6 +170,37 @@ int mkc_jit_lane(void *hv, uint32_t cap, int soo, int force_machine, uint32_t *n
     if (src.size() + 1 > out_len) return -1;
     memcpy(out, src.c_str(), src.size() + 1);
     return rc;
+}
+
+// The tier a launch with the default budget lands on, decided as the
+// product library decides it (mk_exec.hip pick_tier, without hiprtc):
+// 3 = native (tis_jit), 2 = compiled schedule (tier 2), 1 = interpreter.
+// `why` gets the shape (tier 3) or the reason for falling back.
+int mkc_tier(void *hv, uint32_t cap, int soo, char *why, size_t why_len)
+{
+    auto *h = (CheckNet *)hv;
+    mk::SchedProgram P;
+    std::string w, src;
+    mk::SchedLimits lim;
+    int tier = 1;
+    if (mk::compile_schedule(h->net, cap, soo != 0, lim, P, w)) {
+        const mk::JitLimits jl = mk::JitLimits::from_env();
+        mk::JitShape sh = mk::JIT_STREAM;
+        bool heavy = false;
+        uint32_t pool = 0;
+        if (mk::jit_lane_source(P, jl, src, w, &sh, nullptr, &heavy, false, &pool)) {
+            tier = 3;
+            w = sh == mk::JIT_MACHINE ? (pool ? "machine-pool" : "machine") : heavy ? "stream-heavy" : "stream";
+        } else {
+            tier = 2;
+        }
+    }
+    if (why && why_len) {
+        const size_t k = std::min(why_len - 1, w.size());
+        memcpy(why, w.data(), k);
+        why[k] = 0;
+    }
+    return tier;
 }
 
 } // extern "C"

@@ -1297,16 +1297,28 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
         size_t used = 0;
         for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1 : 0;
         const size_t bytes = 8 * used + 16;
-        uint32_t m = lim.pool ? lim.pool : (uint32_t)std::min<size_t>(kJitPoolMaxSlots, kJitPoolBytes / bytes / 64 * 64);
-        m = m / 64 * 64;
-        const bool ok = s == JIT_MACHINE && lim.compact && g.entry.size() <= kJitPoolMaxVariants &&
-                        m >= (lim.pool ? 64u : kJitPoolMinSlots) && m <= 4096 && bytes * m <= 65536;
-        *pool = ok ? m : 0;
+        uint32_t m = 0;
+        if (s == JIT_MACHINE && lim.compact) {
+            if (lim.pool >= 64) { // LDS pool of that many slots per wave (experiments)
+                m = lim.pool / 64 * 64;
+                if (g.entry.size() > kJitPoolMaxVariants || m > 4096 || bytes * m > 65536) m = 0;
+            } else if (lim.pool >= 2 && lim.pool <= 8) { // K lanes per thread, as asked
+                m = lim.pool;
+            } else if (lim.pool == 0) { // K lanes per thread by lane state size (VGPRs)
+                m = used <= 6 ? 4 : used <= 12 ? 2 : 0;
+            }
+        }
+        *pool = m;
     }
     if (s == JIT_MACHINE)
         emit_machine_lane(p, g, e);
     else
         emit_stream(p, g, e, max_fast_steps(p, g), checked);
+    if (!checked && e.s.size() > lim.max_src_bytes) {
+        why = "lane source of " + std::to_string(e.s.size()) + " B exceeds the native tier's compile bound (" +
+              std::to_string(lim.max_src_bytes) + " B)";
+        return false;
+    }
     if (shape) *shape = s;
     if (max_steps) *max_steps = s == JIT_STREAM ? max_fast_steps(p, g) : UINT64_MAX;
     if (heavy) *heavy = g.ndops > lim.heavy_ops;
@@ -1700,11 +1712,130 @@ extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
 }
 )";
 
+// Kernel of the machine shape with K lanes per thread (MK_KLANES): lane
+// compaction in registers.  Each thread holds MK_KLANES lanes (Q[]); a wave
+// turn picks the lowest superblock variant u any of its 64 x K lanes sits on,
+// every thread activates one of its lanes on u (if it has one) and mk_run(u)
+// runs them together.  For a self-loop the loop leaves once a quarter of the
+// group has left (MK_LOOP_NEED), and each thread whose lane left swaps in
+// another of its lanes waiting on u; the loop runs on while that keeps at
+// least half of the wave busy (or nothing else is runnable).  So a loop's
+// lanes are replaced as they finish instead of idling until the wave's
+// longest trip ends, with no memory traffic: the swap is a select over K
+// register copies.  Lanes that end answer their input; once MK_REFILL_MIN of
+// the wave's lanes have ended (or nothing else can run) they take new
+// inputs, dealt from the wave's chunks of 64 (chunk c of wave w: w + c*nw).
+// Stack slots belong to (thread, lane slot): column gid * K + k, stride
+// p.lanes = threads * K.
+static const char *const kMachineMultiKernel = R"(
+#define MK_REFILL_MIN 64u
+#define MK_SB_FREE 0xFFFFFFFDu // answered: the slot waits for a new input
+MK_FN uint32_t mk_rank64(unsigned long long b)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+// The K lane slots are separate variables Q0, Q1, ... (MK_EACH(F) expands
+// F(0) F(1) ...): a register array indexed in a loop stays in scratch.
+#define MK_GET(j) if (k == j##u) L = Q##j;
+#define MK_PUT(j) if (k == j##u) Q##j = L;
+#define MK_FIND(j) if (k == MK_KLANES && Q##j.sb == u && j##u != skip) k = j##u;
+
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t gw = gid >> 6, nw = ((uint64_t)gridDim.x * 256u) >> 6;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+#define MK_DECL(j) MkLane Q##j; uint64_t qi##j;
+    MK_EACH(MK_DECL)
+    // the wave's input stream: chunk c of this wave covers [(gw + c*nw) * 64, +64)
+    uint64_t spos = 0; // inputs of the wave's stream handed out so far (uniform)
+#define MK_IDX(pos) ((gw + ((pos) >> 6) * nw) * 64u + ((pos) & 63u))
+#define MK_FIRST(j) { const uint64_t i = MK_IDX(spos + lane); spos += 64u; \
+        mk_init(Q##j, i < p.n ? sched_input(p, i) : 0); if (i >= p.n) Q##j.sb = MK_SB_IDLE; qi##j = i; }
+    MK_EACH(MK_FIRST)
+    int32_t *const sbase = p.slots ? p.slots + gid * MK_KLANES : (int32_t *)0;
+    MkLane L;
+    mk_init(L, 0);
+    for (;;) {
+        // retire ended lanes; refill them once enough have ended or nothing else runs
+        uint32_t runnable = MK_SB_IDLE, ndone = 0;
+#define MK_RETIRE(j) \
+        if (Q##j.sb == MK_SB_DONE) { \
+            p.out[qi##j] = (Q##j.st & MK_ST_HAS_OUTPUT) ? Q##j.outv : 0; \
+            p.status[qi##j] = (uint8_t)Q##j.st; \
+            if (p.steps) p.steps[qi##j] = Q##j.steps; \
+            count_lane(cnt, Q##j.steps, Q##j.st); \
+            Q##j.sb = MK_SB_FREE; \
+        } \
+        ndone += Q##j.sb == MK_SB_FREE ? 1u : 0u; \
+        runnable = Q##j.sb < MK_SB_FREE && Q##j.sb < runnable ? Q##j.sb : runnable;
+        MK_EACH(MK_RETIRE)
+        const uint32_t wdone = (uint32_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(ndone));
+        const uint32_t umin = MK_WAVE_MIN(runnable);
+        if (wdone && (wdone >= MK_REFILL_MIN || umin >= MK_SB_FREE) && spos < (uint64_t)1 << 62) {
+            bool more = false;
+#define MK_REFILL(j) { \
+            const bool want = Q##j.sb == MK_SB_FREE; \
+            const unsigned long long b = __ballot(want); \
+            const uint64_t i = MK_IDX(spos + mk_rank64(b)); \
+            spos += (uint64_t)__popcll(b); \
+            if (want) { \
+                if (i < p.n) { mk_init(Q##j, sched_input(p, i)); qi##j = i; } \
+                else Q##j.sb = MK_SB_IDLE; \
+            } \
+            more = more || (want && i < p.n); }
+            MK_EACH(MK_REFILL)
+            if (!__ballot(more)) spos = (uint64_t)1 << 62; // the wave's stream is exhausted
+            continue;
+        }
+        if (umin >= MK_SB_FREE) break; // nothing runnable, nothing to refill
+        const uint32_t u = umin;
+        const bool loop = mk_is_loop(u);
+        uint32_t k = MK_KLANES, skip = MK_KLANES;
+        MK_EACH(MK_FIND)
+        bool has = k < MK_KLANES;
+        MK_EACH(MK_GET)
+        for (;;) {
+            // loop variants: the group's largest step count (exec is full here)
+            const uint32_t smax = loop ? MK_WAVE_MAX(has ? L.steps : 0u) : 0u;
+            const uint32_t pol = (12u << 8) | (1u << 16); // a loop leaves at a quarter of its lanes gone
+            if (has) mk_run(u, L, p.budget, sbase ? sbase + k : (int32_t *)0, p.lanes, pol, smax);
+            MK_EACH(MK_PUT)
+            if (!loop) break;
+            // threads whose lane left u swap in another of their lanes on u
+            if (has && L.sb != u) {
+                skip = k;
+                k = MK_KLANES;
+                MK_EACH(MK_FIND)
+                has = k < MK_KLANES;
+                MK_EACH(MK_GET)
+            }
+            const uint32_t nin = (uint32_t)__popcll(__ballot(has));
+            if (nin == 0u) break;
+            if (nin < 32u) { // under half the wave: leave if anything else could run
+                bool other = false;
+#define MK_OTHER(j) other = other || (Q##j.sb != u && Q##j.sb < MK_SB_FREE);
+                MK_EACH(MK_OTHER)
+                if (__ballot(other)) break;
+            }
+        }
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+)";
+
 std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
                               uint32_t pool)
 {
     Emitter e;
-    if (shape == JIT_MACHINE && pool) e.line("#define MK_POOL %uu", pool);
+    if (shape == JIT_MACHINE && pool >= 64) e.line("#define MK_POOL %uu", pool);
+    else if (shape == JIT_MACHINE && pool >= 2) {
+        e.line("#define MK_KLANES %uu", pool);
+        std::string each = "#define MK_EACH(F)";
+        for (uint32_t j = 0; j < pool; ++j) each += " F(" + std::to_string(j) + ")";
+        e.line("%s", each.c_str());
+    }
     // hiprtc declares the fixed-width integer types in __hip_internal only
     e.line("typedef __hip_internal::int8_t int8_t;");
     e.line("typedef __hip_internal::uint8_t uint8_t;");
@@ -1774,13 +1905,17 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // max over the wave (ockl's DPP reduction: needs the whole wave active), as a scalar
     e.line("extern \"C\" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);");
     e.line("#define MK_WAVE_MAX(x) __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32((uint32_t)(x)))");
+    e.line("extern \"C\" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);");
+    e.line("extern \"C\" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);");
+    e.line("#define MK_WAVE_MIN(x) __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32((uint32_t)(x)))");
     e.line("#define MK_KEEP(m, need) mk_keep(m, need)");
     e.s += kDeviceCommon;
     e.s += "\n";
     e.s += lane_src;
-    e.s += shape == JIT_MACHINE ? (pool ? kMachinePoolKernel : kMachineKernel)
-           : heavy                ? kStreamKernelHeavy
-                                  : kStreamKernel;
+    const char *mk = kMachineKernel;
+    if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
+    else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;
+    e.s += shape == JIT_MACHINE ? mk : heavy ? kStreamKernelHeavy : kStreamKernel;
     return e.s;
 }
 

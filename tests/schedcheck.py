@@ -27,6 +27,7 @@ def lib():
                                   C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
         h.mkc_jit_lane.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
+        h.mkc_tier.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_char_p, C.c_size_t]
         _lib = h
     return _lib
 
@@ -89,5 +90,19 @@ def emulate(nodes, xs, *, budget=None, stack_cap=None, stop_on_output=False, wan
             raise NotCompiled(why.value.decode())
         assert rc == 0, f"emulator error {rc}"
         return (out, st, sp, plan.value.decode() if plan is not None else None)
+    finally:
+        lib().mkc_free(h)
+
+
+TIERS = {3: "native", 2: "compiled", 1: "interp"}
+
+
+def tier(nodes, *, stack_cap=None, stop_on_output=False):
+    """(tier name, shape or fallback reason) as the product picks it for the default budget."""
+    h, _keep = _load(nodes)
+    try:
+        why = C.create_string_buffer(1024)
+        t = lib().mkc_tier(h, 1024 if stack_cap is None else stack_cap, 1 if stop_on_output else 0, why, len(why))
+        return TIERS[t], why.value.decode()
     finally:
         lib().mkc_free(h)

@@ -89,15 +89,18 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
 # loops), once on the default path and once with the machine shape and a
 # policy that leaves loops early (so groups re-enter loops with smaller
 # and mixed step counts).
-@pytest.mark.parametrize("variant", ["auto", "machine-early-exit", "pool64"])
+@pytest.mark.parametrize("variant", ["auto", "machine-early-exit", "pool64", "k2"])
 def test_loop_phases_bit_exact(gpu, monkeypatch, variant):
     if variant == "machine-early-exit":  # the pool-less kernel, leaving loops early
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
         monkeypatch.setenv("MK_JIT_COMPACT", "0")
         monkeypatch.setenv("MK_JIT_POLICY", "8,12,16")
-    if variant == "pool64":  # the smallest lane pool: groups refill from few parked lanes
+    if variant == "pool64":  # the smallest LDS lane pool: groups refill from few parked lanes
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
         monkeypatch.setenv("MK_JIT_POOL", "64")
+    if variant == "k2":  # two lanes per thread
+        monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+        monkeypatch.setenv("MK_JIT_POOL", "2")
     for label, nodes, xs, kw in loop_cases(n=4096):
         xs = np.asarray(xs, np.int64)
         assert_same(mk.Network(nodes).compute_batch(xs, **kw), oracle(nodes, xs, **kw), f"{label} {variant}")
@@ -425,12 +428,12 @@ def test_wide_immediates_on_symbolic_acc(gpu, mode):
 # its kernels: the lane-pool kernel (compaction; default, and with pools of
 # 64 / 128 slots) and the pool-less one under several wave policies
 # (MK_JIT_POLICY, compiled into each new network's kernel).
-@pytest.mark.parametrize("policy", ["pool", "pool64", "pool128", "8,12,16", "1,0,64", "64,16,1", "16,8,4"])
+@pytest.mark.parametrize("policy", ["k", "k2", "k3", "pool64", "pool128", "8,12,16", "1,0,64", "64,16,1", "16,8,4"])
 def test_machine_shape_and_policies(gpu, monkeypatch, policy):
     monkeypatch.setenv("MK_JIT_SHAPE", "machine")
-    if policy.startswith("pool"):
-        if policy != "pool":
-            monkeypatch.setenv("MK_JIT_POOL", policy[4:])
+    if policy.startswith("pool") or policy.startswith("k"):
+        if policy not in ("k",):
+            monkeypatch.setenv("MK_JIT_POOL", policy.lstrip("pokl"))
     else:
         monkeypatch.setenv("MK_JIT_COMPACT", "0")
         monkeypatch.setenv("MK_JIT_POLICY", policy)
@@ -449,6 +452,7 @@ def test_machine_shape_and_policies(gpu, monkeypatch, policy):
         if label.startswith("c"):
             assert "shape=machine" in plan, plan
             assert ("-pool" in plan) == policy.startswith("pool"), plan
+            assert ("-k" in plan) == (policy.startswith("k") and "machine-k" in plan), plan
         assert_same(got, oracle(nodes, xs, **kw), f"{label} policy {policy}")
 
 
