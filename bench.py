@@ -482,7 +482,7 @@ def main():
             "model": "executed VALU lane-ops per launch (PMC SQ_INSTS_VALU x 64) / launch time",
             "valu_lane_ops_per_instr": prof.get("valu_lane_ops_per_instr"),
             "salu_per_instr": prof.get("salu_per_instr"),
-            "valu_lane_util_norm": prof.get("valu_lane_util_norm"),
+            "valu_lane_util": prof.get("valu_lane_util"),
             "k_model_frac": K_LANE_OPS * instr_per_launch / launch_max / peak,
             "peak_spec": SPEC_LANE_OPS / 1e12,
             "peak_measured": None if peak_meas is None else peak_meas / 1e12,

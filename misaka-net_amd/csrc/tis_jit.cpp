@@ -1298,14 +1298,12 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
         for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1 : 0;
         const size_t bytes = 8 * used + 16;
         uint32_t m = 0;
-        if (s == JIT_MACHINE && lim.compact) {
-            if (lim.pool >= 64) { // LDS pool of that many slots per wave (experiments)
+        if (s == JIT_MACHINE) {
+            if (lim.pool >= 64) { // LDS pool of that many slots per wave
                 m = lim.pool / 64 * 64;
                 if (g.entry.size() > kJitPoolMaxVariants || m > 4096 || bytes * m > 65536) m = 0;
-            } else if (lim.pool >= 2 && lim.pool <= 8) { // K lanes per thread, as asked
+            } else if (lim.pool >= 2 && lim.pool <= 8) { // K lanes per thread
                 m = lim.pool;
-            } else if (lim.pool == 0) { // K lanes per thread by lane state size (VGPRs)
-                m = used <= 6 ? 4 : used <= 12 ? 2 : 0;
             }
         }
         *pool = m;
@@ -1525,7 +1523,6 @@ JitLimits JitLimits::from_env()
     if (!l.slot_bytes) l.slot_bytes = kJitSlotBytes;
     flag("MK_JIT_SLOT_NT", l.slot_nt);
     flag("MK_JIT_IO_NT", l.io_nt);
-    flag("MK_JIT_COMPACT", l.compact);
     num("MK_JIT_POOL", l.pool);
     return l;
 }
@@ -1534,9 +1531,9 @@ std::string JitLimits::key() const
 {
     char b[256];
     snprintf(b, sizeof b,
-             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,compact=%d,pool=%u",
+             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
-             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, (int)compact, pool);
+             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool);
     return b;
 }
 

@@ -69,12 +69,13 @@ struct JitLimits {
     size_t prefetch = kJitPrefetchLoads;   // MK_JIT_PREFETCH (0: off)
     size_t heavy_ops = kJitHeavyOps;       // MK_JIT_HEAVY_OPS
     uint64_t slot_bytes = kJitSlotBytes;   // MK_JIT_SLOT_BYTES
-    // Lane compaction in the machine shape (kMachinePoolKernel): each wave
-    // parks lanes between superblocks in an LDS pool and runs full groups of
-    // lanes that sit on the same superblock.  MK_JIT_COMPACT=0: the pool-less
-    // kernel (generations); MK_JIT_POOL=<slots per wave, multiple of 64>
-    // overrides the size (0: from the lane state size, kJitPoolBytes).
-    bool compact = true;
+    // Lane compaction in the machine shape (experiments, MK_JIT_POOL):
+    //   0     the pool-less kernel, generations (default: fastest measured);
+    //   2..8  K lanes per thread in registers, swapped at loop heads
+    //         (kMachineMultiKernel);
+    //   >=64  an LDS pool of that many parked lanes per wave, largest-group
+    //         dispatch (kMachinePoolKernel).
+    // Both compaction kernels are bit-exact and slower on C5.
     uint32_t pool = 0;
 
     static JitLimits from_env();

@@ -93,7 +93,6 @@ def test_c4_deep_stacks_spill_to_hbm(gpu, mode, depth):
 def test_loop_phases_bit_exact(gpu, monkeypatch, variant):
     if variant == "machine-early-exit":  # the pool-less kernel, leaving loops early
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
-        monkeypatch.setenv("MK_JIT_COMPACT", "0")
         monkeypatch.setenv("MK_JIT_POLICY", "8,12,16")
     if variant == "pool64":  # the smallest LDS lane pool: groups refill from few parked lanes
         monkeypatch.setenv("MK_JIT_SHAPE", "machine")
@@ -424,18 +423,16 @@ def test_wide_immediates_on_symbolic_acc(gpu, mode):
 
 # The native tier's two kernel shapes (tis_jit.h): acyclic schedules stream,
 # cyclic ones run as per-lane state machines.  Force the machine shape on
-# every network (the knobs are read when a network is loaded) and run both of
-# its kernels: the lane-pool kernel (compaction; default, and with pools of
-# 64 / 128 slots) and the pool-less one under several wave policies
-# (MK_JIT_POLICY, compiled into each new network's kernel).
-@pytest.mark.parametrize("policy", ["k", "k2", "k3", "pool64", "pool128", "8,12,16", "1,0,64", "64,16,1", "16,8,4"])
+# every network (the knobs are read when a network is loaded) and run each of
+# its kernels: the pool-less one under several wave policies (MK_JIT_POLICY,
+# compiled into each new network's kernel) and the two lane-compaction
+# kernels (MK_JIT_POOL: K lanes per thread, or an LDS pool per wave).
+@pytest.mark.parametrize("policy", ["k2", "k4", "pool64", "pool256", "8,12,16", "1,0,64", "64,16,1", "16,8,4"])
 def test_machine_shape_and_policies(gpu, monkeypatch, policy):
     monkeypatch.setenv("MK_JIT_SHAPE", "machine")
     if policy.startswith("pool") or policy.startswith("k"):
-        if policy not in ("k",):
-            monkeypatch.setenv("MK_JIT_POOL", policy.lstrip("pokl"))
+        monkeypatch.setenv("MK_JIT_POOL", policy.lstrip("pokl"))
     else:
-        monkeypatch.setenv("MK_JIT_COMPACT", "0")
         monkeypatch.setenv("MK_JIT_POLICY", policy)
     cases = [("c2", mk.networks.example_network(), po.gen_inputs(SEED, 5000), {}),
              ("c3", mk.networks.sample_network(), po.gen_inputs(SEED, 5000), {}),
@@ -452,7 +449,7 @@ def test_machine_shape_and_policies(gpu, monkeypatch, policy):
         if label.startswith("c"):
             assert "shape=machine" in plan, plan
             assert ("-pool" in plan) == policy.startswith("pool"), plan
-            assert ("-k" in plan) == (policy.startswith("k") and "machine-k" in plan), plan
+            assert ("machine-k" in plan) == policy.startswith("k"), plan
         assert_same(got, oracle(nodes, xs, **kw), f"{label} policy {policy}")
 
 

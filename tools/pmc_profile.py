@@ -77,9 +77,9 @@ for cfg in cfgs:
         out["valu_lane_ops_per_instr"] = s["SQ_INSTS_VALU"] * 64 / retired
         out["salu_per_instr"] = s.get("SQ_INSTS_SALU", 0) / retired
         if s.get("SQ_ACTIVE_INST_VALU"):
-            # rocprof's VALU utilisation reads half the active-lane fraction on
-            # gfx950 (C2 / C4, whose lanes never diverge, read 0.48-0.50): x2
-            out["valu_lane_util_norm"] = 2 * s["SQ_THREAD_CYCLES_VALU"] / (s["SQ_ACTIVE_INST_VALU"] * 64)
+            # active lanes per issued VALU wave-instruction (rocprof's VALU
+            # utilisation): C2 / C4, whose lanes never diverge, read 0.96-1.0
+            out["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (s["SQ_ACTIVE_INST_VALU"] * 64)
     with open(os.path.join("profiles", f"pmc_{workload}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
