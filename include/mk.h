@@ -9,8 +9,11 @@
  *
  * Thread safety: every call is safe to make concurrently on one mk_net
  * (Go net/http runs /compute handlers concurrently, master.go:197).  The host
- * API serialises per handle; the device API is stream-ordered and callers
- * that issue it concurrently on one handle and device must share one stream.
+ * API serialises per handle.  Launches of one handle on one device share its
+ * scratch (stack slots, counters), so the library orders them across
+ * streams: work enqueued on a stream other than the previous launch's waits
+ * for that launch (the host API's internal stream included).  Callers that
+ * never change stream pay nothing for it.
  */
 #ifndef MK_H
 #define MK_H
@@ -194,6 +197,27 @@ int mk_stats_fold(mk_net *net, int device, uint64_t *d_stats, void *stream);
 /* Fill d_out[i] = gen(seed, offset + i) on device (same generator as MK_IN_GEN). */
 int mk_generate_inputs_device(int device, uint64_t seed, uint32_t gen_kind, uint32_t gen_mask,
                               uint64_t offset, size_t n, int32_t *d_out, void *stream);
+
+/* ---- lane trace -------------------------------------
+ * The reference logs every instruction it executes (log.Printf of tokens,
+ * ACC, BAK; program.go:222-223).  mk_trace_lane runs ONE /compute input
+ * through the bytecode interpreter (tier 1, the tier that executes one TIS
+ * instruction at a time) on `device` and returns its first max_entries
+ * retired instructions in schedule order: round, program node (index in
+ * sorted-name order), the ptr it executed at, ACC and BAK after it -- the
+ * same records as the oracle's orc_trace_lane, so a lane whose result
+ * differs can be diffed instruction by instruction.  *count = entries
+ * written, *status = the lane's MK_ST_* byte.  Synchronous. */
+typedef struct {
+    uint32_t round;
+    uint16_t node;
+    uint16_t ip;
+    int64_t acc;
+    int64_t bak;
+} mk_trace_entry;
+
+int mk_trace_lane(mk_net *net, int device, int64_t input, const mk_opts *opts, mk_trace_entry *out,
+                  uint32_t max_entries, uint32_t *count, uint8_t *status);
 
 /* ---- introspection -------------------------------------------------------- */
 /* Token dump of one program in the test format: lines joined by '\n', tokens

@@ -121,6 +121,8 @@ SIGNATURES = {
     "mk_net_prepare": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_int]),
     "mk_net_jit_source": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
     "mk_valu_probe_device": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
+    "mk_trace_lane": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.POINTER(mk_opts), C.c_void_p, C.c_uint32,
+                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]),
     "mk_version": (C.c_char_p, []),
 }
 

@@ -71,6 +71,9 @@ struct KParams {
     uint32_t spill_rows; // stack_cap - ring (HBM entries per stack per lane)
     int32_t *spill;      // [nstack][spill_rows][lanes]
     uint64_t lanes;      // resident lanes (grid threads)
+    mk_trace_entry *trace; // lane trace of input 0 (mk_trace_lane), or null
+    uint32_t trace_max;
+    uint32_t *trace_n;   // entries written (device)
 };
 
 
@@ -153,6 +156,7 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
 
     uint64_t idx = gid;
     bool active = idx < p.n;
+    uint32_t round = 0, ntrace = 0; // lane trace: rounds of input 0 and entries written
 
     auto init = [&](uint64_t i) {
 #pragma unroll
@@ -184,15 +188,27 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
                 const Insn I = fetch(code, p.base[n] + (uint32_t)u); // one s_load_dwordx4
                 if (!mine) continue;
                 pending = false;
+                auto record = [&]() { // mk_trace_lane: one entry per retired instruction of input 0
+                    if (p.trace && idx == 0 && ntrace < p.trace_max) {
+                        mk_trace_entry &e = p.trace[ntrace++];
+                        e.round = round;
+                        e.node = (uint16_t)n;
+                        e.ip = (uint16_t)u;
+                        e.acc = acc[n];
+                        e.bak = bak[n];
+                    }
+                };
                 auto retire = [&]() {
                     ip[n] = (ip[n] + 1 == (int32_t)len) ? 0 : ip[n] + 1; // program.go:429
                     ++steps;
                     changed = true;
+                    record();
                 };
                 auto jump = [&](int32_t t) {
                     ip[n] = t;
                     ++steps;
                     changed = true;
+                    record();
                 };
                 switch (I.op) {
                 case OP_NOP: retire(); break;
@@ -309,6 +325,8 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
             if (!changed) { done = true; reason = MK_ST_QUIESCENT; }
             else if (steps >= p.budget) { done = true; reason = MK_ST_BUDGET; }
         }
+        ++round;
+        if (done && p.trace && idx == 0) *p.trace_n = ntrace;
         if (done) {
             const uint32_t st = reason | (out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0u);
             p.out[idx] = out_cnt > 0 ? out_val : 0;
@@ -1126,6 +1144,14 @@ struct DevCtx {
     unsigned long long *d_partials = nullptr; // per-wave counters
     size_t partials_bytes = 0;
     hipStream_t stream = nullptr;
+    // The handle's per-device scratch (stack slots, spill rows, counters,
+    // staging) is shared by every stream that launches on it: the host API
+    // uses `stream`, the device API the caller's.  Work is ordered across a
+    // change of stream (order_on): the new stream waits for an event
+    // recorded on the previous one.
+    hipStream_t last = nullptr;
+    bool used = false;
+    hipEvent_t ev = nullptr;
 };
 
 } // namespace mk
@@ -1157,6 +1183,7 @@ struct mk_net {
                 if (sc->jit.dev[d].mod) (void)hipModuleUnload(sc->jit.dev[d].mod);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
+            if (c.ev) (void)hipEventDestroy(c.ev);
         }
         (void)hipSetDevice(prev);
     }
@@ -1198,7 +1225,23 @@ int ensure_device(mk_net *h, int d)
     if (hipMemcpy(c.d_code, h->net.code.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return MK_EDEVICE;
     if (hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) return MK_EDEVICE;
     if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) return MK_EDEVICE;
+    if (hipEventCreateWithFlags(&c.ev, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
     c.ready = true;
+    return MK_OK;
+}
+
+// Caller holds h->mu, device d current.  Work about to be enqueued on `s`
+// that touches the handle's scratch on this device: if the previous such
+// work went to another stream, `s` first waits for it.  Free when the
+// stream does not change (the bench's and the master's steady state).
+int order_on(DevCtx &c, hipStream_t s)
+{
+    if (c.used && c.last != s) {
+        if (hipEventRecord(c.ev, c.last) != hipSuccess || hipStreamWaitEvent(s, c.ev, 0) != hipSuccess)
+            return MK_EDEVICE;
+    }
+    c.used = true;
+    c.last = s;
     return MK_OK;
 }
 
@@ -1649,13 +1692,15 @@ Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, uint32_t budget, SchedCa
 
 // Caller holds h->mu.  Asynchronous on `stream`.
 int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,
-                  uint32_t *d_steps, uint64_t *d_stats, const mk_opts *o, hipStream_t stream)
+                  uint32_t *d_steps, uint64_t *d_stats, const mk_opts *o, hipStream_t stream,
+                  mk_trace_entry *trace = nullptr, uint32_t trace_max = 0, uint32_t *trace_n = nullptr)
 {
     if (n == 0) return MK_OK;
     int rc = ensure_device(h, d);
     if (rc) return rc;
     DevCtx &c = h->dev[d];
     DeviceGuard g(d);
+    if ((rc = order_on(c, stream))) return rc;
     uint32_t budget, cap, flags;
     resolve_opts(o, budget, cap, flags);
     SchedCache *sc = nullptr;
@@ -1711,6 +1756,9 @@ int launch_locked(mk_net *h, int d, const mk_input *in, size_t n, int32_t *d_out
     p.spill_rows = spill_rows;
     p.spill = c.d_spill;
     p.lanes = lanes;
+    p.trace = trace;
+    p.trace_max = trace_max;
+    p.trace_n = trace_n;
     const Insn *code = c.d_code;
     void *args[] = {(void *)&code, (void *)&p};
     if (hipLaunchKernel(L.fn, dim3(L.blocks), dim3(kBlock), args, L.lds, stream) != hipSuccess)
@@ -2061,6 +2109,48 @@ int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *
 
 void mk_session_free(mk_session *s) { delete s; }
 
+int mk_trace_lane(mk_net *h, int device, int64_t input, const mk_opts *opts, mk_trace_entry *out,
+                  uint32_t max_entries, uint32_t *count, uint8_t *status)
+{
+    if (!h || !count || !status || (max_entries && !out)) return MK_EINVAL;
+    const int ndev = mk::device_count();
+    if (ndev <= 0) return MK_EDEVICE;
+    if (device < 0 || device >= ndev || device >= mk::kMaxDevices) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = mk::ensure_device(h, device);
+    if (rc) return rc;
+    mk::DevCtx &c = h->dev[device];
+    mk::DeviceGuard g(device);
+    // one lane on the bytecode interpreter (tier 1), the only tier that
+    // executes one TIS instruction at a time
+    mk_opts o{};
+    if (opts) o = *opts;
+    o.flags = (o.flags & MK_FLAG_STOP_ON_OUTPUT) | MK_FLAG_FORCE_INTERP;
+    const size_t tb = (size_t)max_entries * sizeof(mk_trace_entry);
+    char *buf = nullptr;
+    if (hipMalloc(&buf, 256 + tb + 64) != hipSuccess) return MK_ENOMEM;
+    int64_t *din = (int64_t *)buf;
+    int32_t *dout = (int32_t *)(buf + 8);
+    uint8_t *dst = (uint8_t *)(buf + 12);
+    uint32_t *dn = (uint32_t *)(buf + 16);
+    mk_trace_entry *dtr = (mk_trace_entry *)(buf + 256);
+    mk_input mi{};
+    mi.kind = MK_IN_I64;
+    mi.data = din;
+    if (hipMemcpyAsync(din, &input, 8, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
+        hipMemsetAsync(dn, 0, 4, c.stream) != hipSuccess)
+        rc = MK_EDEVICE;
+    if (!rc) rc = mk::launch_locked(h, device, &mi, 1, dout, dst, nullptr, nullptr, &o, c.stream, dtr, max_entries, dn);
+    if (!rc && (hipMemcpyAsync(count, dn, 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+                hipMemcpyAsync(status, dst, 1, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+                hipStreamSynchronize(c.stream) != hipSuccess))
+        rc = MK_EDEVICE;
+    if (!rc && *count && hipMemcpy(out, dtr, (size_t)*count * sizeof(mk_trace_entry), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = MK_EDEVICE;
+    (void)hipFree(buf);
+    return rc;
+}
+
 int mk_stats_fold(mk_net *h, int device, uint64_t *d_stats, void *stream)
 {
     if (!h || !d_stats) return MK_EINVAL;
@@ -2072,6 +2162,7 @@ int mk_stats_fold(mk_net *h, int device, uint64_t *d_stats, void *stream)
     if (rc) return rc;
     mk::DevCtx &c = h->dev[device];
     mk::DeviceGuard g(device);
+    if ((rc = mk::order_on(c, (hipStream_t)stream))) return rc;
     if ((rc = mk::ensure_partials(c, 0))) return rc;
     return mk::launch_stats_reduce(c, d_stats, (hipStream_t)stream);
 }

@@ -250,6 +250,20 @@ class Network:
         launch.keep = (mi, o, self)
         return launch
 
+    TRACE_DTYPE = np.dtype([("round", "<u4"), ("node", "<u2"), ("ip", "<u2"), ("acc", "<i8"), ("bak", "<i8")])
+
+    def trace(self, value, *, max_entries=4096, budget=None, stack_cap=None, stop_on_output=False, device=0):
+        """Lane trace of one /compute input (mk_trace_lane): the first
+        ``max_entries`` retired instructions as a structured array
+        (round, node, ip, acc, bak) and the lane's status byte."""
+        out = np.zeros(max_entries, self.TRACE_DTYPE)
+        cnt = C.c_uint32()
+        st = C.c_uint8()
+        o = make_opts(budget, stack_cap, stop_on_output)
+        N.check(N.lib().mk_trace_lane(self._h, device, int(value), C.byref(o), out.ctypes.data_as(C.c_void_p),
+                                      max_entries, C.byref(cnt), C.byref(st)), "mk_trace_lane")
+        return out[: cnt.value], st.value
+
     def sessions(self, n, *, device=0, budget=None, stack_cap=None) -> "SessionSet":
         """``n`` stateful instances of this network (row f2, :class:`SessionSet`)."""
         return SessionSet(self, n, device=device, budget=budget, stack_cap=stack_cap)

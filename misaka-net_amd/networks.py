@@ -135,6 +135,45 @@ def countdown_network():
     ]
 
 
+# ---- census classes (tests/test_tier_census.py, bench.py --config t_*) ---------
+# Network shapes that stress the schedule compiler: control state that
+# depends on the data through stack depths, many JRO arms, many nodes.
+def census_classes():
+    """{class: [(label, nodes, input kwargs for oracle.gen_inputs)]} -- shapes
+    whose control state the schedule compiler may not bound (tests/
+    test_tier_census.py; bench.py --config t_*)."""
+    P = lambda name, text: NodeSpec(name, "program", text)  # noqa: E731
+    S = lambda name: NodeSpec(name, "stack", "")  # noqa: E731
+    # push x (0..255) values then pop them all: stack depth follows the data
+    dyn_depth = [P("a", "IN ACC\nSAV\nJEZ E\nL: PUSH ACC, s\nSUB 1\nJGZ L\nSWP\nM: POP s, NIL\nSUB 1\nJGZ M\n"
+                      "E: MOV 7, ACC\nOUT ACC"), S("s")]
+    # two stacks, depths x & 15 and (x >> 4) & 15, popped into a sum
+    two_stacks = [P("a", "IN ACC\nSAV\nMOV 0, ACC\nMOV ACC, a:R1\nSWP\nSAV\n"
+                       "A: JEZ B\nPUSH ACC, s\nSUB 1\nJMP A\n"
+                       "B: SWP\nSAV\nC: JEZ D\nPUSH ACC, t\nSUB 1\nJMP C\n"
+                       "D: MOV R1, ACC\nOUT ACC"), S("s"), S("t")]
+    # JRO-heavy: a dispatch loop over x & 7 with 8 arms, x >> 3 rounds
+    arms = "\n".join(f"ADD {k + 1}\nJMP N" for k in range(8))
+    jro_heavy = [P("a", "IN ACC\nSAV\nL: SWP\nJEZ E\nSUB 1\nSWP\nADD 3\nSAV\nJRO 2\n" + arms +
+                   "\nN: SWP\nSAV\nSWP\nJMP L\nE: SWP\nOUT ACC")]
+    # 16 program nodes in a ring: each adds its index and forwards; node 0 outputs
+    ring = []
+    for k in range(16):
+        nxt = f"n{(k + 1) % 16:02d}"
+        if k == 0:
+            ring.append(P("n00", f"IN ACC\nMOV ACC, {nxt}:R0\nMOV R1, ACC\nOUT ACC"))
+        elif k == 15:
+            ring.append(P(f"n{k:02d}", f"MOV R0, ACC\nADD {k}\nMOV ACC, n00:R1"))
+        else:
+            ring.append(P(f"n{k:02d}", f"MOV R0, ACC\nADD {k}\nMOV ACC, {nxt}:R0"))
+    return {
+        "data_dependent_stack_depth": [("dyn_depth", dyn_depth, dict(kind=1, mask=255))],
+        "two_stacks_independent_depths": [("two_stacks", two_stacks, dict(kind=1, mask=255))],
+        "jro_heavy": [("jro_heavy", jro_heavy, dict(kind=1, mask=1023))],
+        "sixteen_nodes": [("ring16", ring, dict(kind=0))],
+    }
+
+
 CONFIGS = {
     "c1_example_cpu": example_network,
     "c2_example": example_network,

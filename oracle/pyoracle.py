@@ -72,6 +72,8 @@ def lib():
         h.orc_sessions_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                            C.c_int]
         h.orc_go_atoi.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64)]
+        h.orc_trace_lane.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_uint32,
+                                     C.POINTER(C.c_uint32)]
         _lib = h
     return _lib
 
@@ -155,6 +157,20 @@ class OracleNet:
         )
         assert rc == 0
         return out, st, sp
+
+
+TRACE_DTYPE = np.dtype([("round", "<u4"), ("node", "<u2"), ("ip", "<u2"), ("acc", "<i8"), ("bak", "<i8")])
+
+
+def trace_lane(net: "OracleNet", x: int, *, max_entries: int = 4096, budget: Optional[int] = None,
+               stack_cap: Optional[int] = None, stop_on_output: bool = False):
+    """Every retired instruction of the lane for input x (round, node, ip,
+    acc, bak after it), first max_entries of them, and the lane's status."""
+    out = np.zeros(max_entries, TRACE_DTYPE)
+    cnt = C.c_uint32()
+    st = lib().orc_trace_lane(net._h, int(x), budget or (1 << 20), 1024 if stack_cap is None else stack_cap,
+                              1 if stop_on_output else 0, out.ctypes.data_as(C.c_void_p), max_entries, C.byref(cnt))
+    return out[: cnt.value], st
 
 
 class OracleSessions:

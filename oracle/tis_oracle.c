@@ -921,6 +921,65 @@ static uint8_t run_lane(const orc_net *net, lane_t *ln, int64_t input, const orc
     }
 }
 
+/* Lane trace (the reference's per-instruction
+ * log.Printf, program.go:222-223, as data): run_lane for one input,
+ * recording every retired instruction -- round, program node (sorted-name
+ * index), the ptr it executed at, ACC and BAK after it -- up to `max`
+ * entries.  Returns the lane status; *count = entries written. */
+typedef struct {
+    uint32_t round;
+    uint16_t node;
+    uint16_t ip;
+    int64_t acc;
+    int64_t bak;
+} orc_trace_entry;
+
+static lane_t *lane_alloc(const orc_net *net, uint32_t cap);
+static void lane_free(const orc_net *net, lane_t *ln);
+
+int orc_trace_lane(const orc_net *net, int64_t input, uint32_t budget, uint32_t stack_cap, int stop_on_output,
+                   orc_trace_entry *out, uint32_t max, uint32_t *count)
+{
+    lane_t *ln = lane_alloc(net, stack_cap);
+    lane_reset(net, ln, input);
+    uint32_t k = 0, round = 0;
+    uint8_t st;
+    for (;;) {
+        int changed = 0, over = 0, stop = 0;
+        for (int n = 0; n < net->nprog; n++) {
+            const int ip = ln->node[n].ptr;
+            int r = attempt(net, ln, n);
+            if (r == R_RETIRED && k < max) {
+                out[k].round = round;
+                out[k].node = (uint16_t)n;
+                out[k].ip = (uint16_t)ip;
+                out[k].acc = ln->node[n].acc;
+                out[k].bak = ln->node[n].bak;
+                k++;
+            }
+            if (r & R_OVERFLOW) {
+                over = 1;
+                break;
+            }
+            changed |= r & R_CHANGED;
+            if (stop_on_output && ln->out_cnt > 0) {
+                stop = 1;
+                break;
+            }
+        }
+        if (over) { st = ST_STACK_OVERFLOW; break; }
+        if (stop) { st = ST_OUTPUT_STOP; break; }
+        if (!changed) { st = ST_QUIESCENT; break; }
+        if (ln->steps >= budget) { st = ST_BUDGET; break; }
+        round++;
+    }
+    if (ln->out_cnt > 0)
+        st |= ST_HAS_OUTPUT;
+    *count = k;
+    lane_free(net, ln);
+    return st;
+}
+
 static lane_t *lane_alloc(const orc_net *net, uint32_t cap)
 {
     lane_t *ln = (lane_t *)calloc(1, sizeof(lane_t));

@@ -554,3 +554,50 @@ def test_session_seq_single_instance_long_burst(gpu):
     o = po.OracleSessions(po.OracleNet(nodes), 1)
     ref = [o.compute([x]) for x in xs.tolist()]
     assert r.out.tolist() == [int(x[0][0]) for x in ref] and r.status.tolist() == [int(x[1][0]) for x in ref]
+
+
+# The device API on a caller's stream and the host API on the handle's own
+# stream share the handle's stack slots and counters: the library orders
+# them (mk_exec.hip order_on), so interleaved launches stay exact.
+def test_device_and_host_api_interleaved_streams(gpu):
+    import torch
+
+    nodes = mk.networks.pipeline_network(64)
+    net = mk.Network(nodes)
+    n = 1 << 16
+    side = torch.cuda.Stream()
+    outs = []
+    for rep in range(3):
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        st = torch.empty(n, dtype=torch.uint8, device="cuda")
+        net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), seed=SEED + rep,
+                           stream=side.cuda_stream)
+        xs = po.gen_inputs(SEED + 100 + rep, 2048)
+        host = net.compute_batch(xs)  # enqueued while the side-stream launch may still run
+        outs.append((out, st, xs, host, rep))
+    torch.cuda.synchronize()
+    for out, st, xs, host, rep in outs:
+        assert_same(host, oracle(nodes, xs), f"host API rep {rep}")
+        tail = po.gen_inputs(SEED + rep, n)[-1024:]
+        ref = oracle(nodes, tail)
+        assert np.array_equal(out.cpu().numpy()[-1024:], ref[0]) and np.array_equal(st.cpu().numpy()[-1024:], ref[1])
+
+
+# Lane trace (mk_trace_lane): the interpreter's record
+# of every retired instruction of one lane equals the oracle's
+# (orc_trace_lane) -- round, node, ptr, ACC and BAK after each instruction.
+@pytest.mark.parametrize("seed", range(0, 40))
+def test_lane_trace_matches_oracle(gpu, seed):
+    if seed < 4:
+        nodes = [mk.networks.example_network, mk.networks.sample_network, mk.networks.countdown_network,
+                 lambda: mk.networks.pipeline_network(8)][seed]()
+    else:
+        nodes = random_network(seed)
+    onet = po.OracleNet(nodes)
+    net = mk.Network(nodes)
+    for x in po.gen_inputs(seed + 17, 3).tolist() + [0, 7]:
+        kw = dict(budget=[37, 200, 5000][seed % 3], stack_cap=[3, 16, 1024][seed % 3])
+        got, st = net.trace(x, max_entries=512, **kw)
+        ref, rst = po.trace_lane(onet, x, max_entries=512, **kw)
+        assert st == rst, (seed, x, st, rst)
+        assert got.tobytes() == ref.tobytes(), (seed, x, got[:8], ref[:8])

@@ -8,6 +8,7 @@ integer semantics (SURVEY.md section 8 row c).
 import numpy as np
 import pytest
 
+import misaka_net_amd as mk
 from oracle import pyoracle as po
 
 Q, B, OV, OS, H = po.ST_QUIESCENT, po.ST_BUDGET, po.ST_STACK_OVERFLOW, po.ST_OUTPUT_STOP, po.ST_HAS_OUTPUT
@@ -159,3 +160,18 @@ def test_generator_edges_every_16th_lane():
     assert all(int(xs[i]) in edges for i in range(15, 64, 16))
     m = po.gen_inputs(0x4D49534B41, 1000, kind=1, mask=1023)
     assert m.min() >= 0 and m.max() <= 1023
+
+
+def test_lane_trace_kat_example_network():
+    # README.md:39-44 network, x = 5: misaka1 IN/ADD 1/MOV, misaka2 MOV/ADD 1/
+    # PUSH/POP/MOV, misaka1 MOV R0/OUT, then both trailing NOPs: 12 retired
+    # instructions in the canonical schedule; ACC after the last OUT is 7
+    t, st = po.trace_lane(po.OracleNet(mk.networks.example_network()), 5)
+    assert st == po.ST_HAS_OUTPUT | po.ST_QUIESCENT
+    assert [(int(e["node"]), int(e["ip"])) for e in t] == [
+        (0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (1, 3), (1, 4), (0, 3), (1, 5), (0, 4), (0, 5)]
+    assert [int(e["acc"]) for e in t] == [5, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7, 7]
+    assert [int(e["round"]) for e in t] == [0, 1, 2, 2, 3, 4, 5, 6, 7, 7, 8, 9]
+    # the trace is bounded by max_entries; the status is still the lane's
+    t2, st2 = po.trace_lane(po.OracleNet(mk.networks.example_network()), 5, max_entries=4)
+    assert len(t2) == 4 and st2 == st
