@@ -32,6 +32,7 @@ extern "C" {
 #define MK_ELIMIT (-3)  /* network exceeds executor limits                */
 #define MK_EDEVICE (-4) /* HIP runtime error / no usable GPU              */
 #define MK_ENOMEM (-5)  /* allocation failed                              */
+#define MK_EBUSY (-6)   /* would block: port full / stack empty (retry)  */
 
 /* ---- limits ------------------------------------------------------------ */
 #define MK_MAX_PROGRAM_NODES 16
@@ -43,6 +44,7 @@ extern "C" {
 #define MK_ST_BUDGET 2         /* retired-instruction budget reached at a round end           */
 #define MK_ST_STACK_OVERFLOW 3 /* a PUSH exceeded stack_cap (reference stacks are unbounded)  */
 #define MK_ST_OUTPUT_STOP 4    /* stopped at the first OUT (MK_FLAG_STOP_ON_OUTPUT)           */
+#define MK_ST_REMOTE_WAIT 5    /* session call parked on remote peers / inbound RPCs (row f4)  */
 #define MK_ST_REASON_MASK 0x0f
 #define MK_ST_HAS_OUTPUT 0x10  /* lane produced a /compute result                              */
 
@@ -54,6 +56,14 @@ extern "C" {
 #define MK_NODE_PROGRAM 0
 #define MK_NODE_STACK 1
 #define MK_NODE_MASTER 2
+/* Peers served outside this executor -- reference nodes of a mixed
+ * deployment (row f4): MOV to a remote program's port, PUSH / POP on a
+ * remote stack become requests a stateful session hands to its host, which
+ * makes the reference's RPC (Program.Send, Stack.Push / Stack.Pop,
+ * messenger.proto:9-28; see mk_session_remote_*).  Batch lanes have no
+ * peers: such an instruction blocks there forever. */
+#define MK_NODE_REMOTE_PROGRAM 3
+#define MK_NODE_REMOTE_STACK 4
 
 typedef struct mk_net mk_net;
 
@@ -183,6 +193,45 @@ int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int3
  * own stream); calls on one session are ordered. */
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
                               uint32_t *d_steps, void *stream);
+
+/* ---- mixed deployments (row f4): sessions of a network with remote peers --
+ * A call on such a session runs until it has its output or nothing more can
+ * happen without the peers; then it is PARKED: status MK_ST_REMOTE_WAIT,
+ * no output, the call still open.  The host then
+ *   - makes the RPC of every outstanding request (mk_session_remote_poll:
+ *     Program.Send to a remote port, Stack.Push / Stack.Pop on a remote stack,
+ *     program.go:475-536) and reports each completion (mk_session_remote_done,
+ *     with the popped value for a pop);
+ *   - serves the peers' RPCs to this instance's nodes: Program.Send into a
+ *     local port (mk_session_port_put, MK_EBUSY while full: program.go:163),
+ *     Stack.Push / Stack.Pop on a local stack (mk_session_stack_push / _pop,
+ *     MK_EBUSY while empty: stack.go:133-155);
+ *   - resumes the call (mk_session_step with in = NULL).
+ * All of these are ordered on the session's stream and synchronous. */
+#define MK_REMOTE_SEND 0
+#define MK_REMOTE_PUSH 1
+#define MK_REMOTE_POP 2
+typedef struct {
+    uint32_t node;   /* local program node (sorted-name index) making the request */
+    uint32_t op;     /* MK_REMOTE_*                                              */
+    uint32_t remote; /* index of the peer among the network's MK_NODE_REMOTE_* nodes */
+    uint32_t reg;    /* MK_REMOTE_SEND: the peer's port R0..R3                   */
+    int32_t value;   /* SEND / PUSH: int32 value                                 */
+} mk_remote_req;
+
+/* One call step on every session: a new /compute call with in[i] (host
+ * arrays), or, with in == NULL, resume each session's parked call. */
+int mk_session_step(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps);
+int mk_session_remote_poll(mk_session *s, size_t inst, mk_remote_req *reqs, int max, int *count);
+int mk_session_remote_done(mk_session *s, size_t inst, uint32_t node, int32_t value);
+int mk_session_port_put(mk_session *s, size_t inst, uint32_t node, uint32_t reg, int32_t value);
+int mk_session_stack_push(mk_session *s, size_t inst, uint32_t stack, int32_t value);
+int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *value);
+
+/* Kind (MK_NODE_*) and index of a node by name: program and stack nodes in
+ * sorted-name order (the canonical schedule), remote peers in declaration
+ * order. */
+int mk_net_node_index(const mk_net *net, const char *name, int *kind, int *index);
 
 /* /reset (master.go:126-143): every session back to the initial state. */
 int mk_session_reset(mk_session *s);

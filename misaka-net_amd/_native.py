@@ -20,17 +20,24 @@ MK_EPARSE = -2
 MK_ELIMIT = -3
 MK_EDEVICE = -4
 MK_ENOMEM = -5
+MK_EBUSY = -6
 
 MK_ST_QUIESCENT = 1
 MK_ST_BUDGET = 2
 MK_ST_STACK_OVERFLOW = 3
 MK_ST_OUTPUT_STOP = 4
+MK_ST_REMOTE_WAIT = 5
 MK_ST_REASON_MASK = 0x0F
 MK_ST_HAS_OUTPUT = 0x10
 
 MK_NODE_PROGRAM = 0
 MK_NODE_STACK = 1
 MK_NODE_MASTER = 2
+MK_NODE_REMOTE_PROGRAM = 3
+MK_NODE_REMOTE_STACK = 4
+MK_REMOTE_SEND = 0
+MK_REMOTE_PUSH = 1
+MK_REMOTE_POP = 2
 
 MK_FLAG_STOP_ON_OUTPUT = 1
 MK_FLAG_FORCE_INTERP = 2
@@ -52,6 +59,7 @@ ERROR_NAMES = {
     MK_ELIMIT: "MK_ELIMIT",
     MK_EDEVICE: "MK_EDEVICE",
     MK_ENOMEM: "MK_ENOMEM",
+    MK_EBUSY: "MK_EBUSY",
 }
 
 
@@ -66,6 +74,11 @@ class mk_opts(C.Structure):
         ("flags", C.c_uint32),
         ("device_mask", C.c_uint32),
     ]
+
+
+class mk_remote_req(C.Structure):
+    _fields_ = [("node", C.c_uint32), ("op", C.c_uint32), ("remote", C.c_uint32), ("reg", C.c_uint32),
+                ("value", C.c_int32)]
 
 
 class mk_input(C.Structure):
@@ -121,6 +134,14 @@ SIGNATURES = {
     "mk_net_prepare": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_int]),
     "mk_net_jit_source": (C.c_int, [C.c_void_p, C.POINTER(mk_opts), C.c_char_p, C.c_size_t]),
     "mk_valu_probe_device": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_void_p]),
+    "mk_session_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mk_session_remote_poll": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(mk_remote_req), C.c_int,
+                                         C.POINTER(C.c_int)]),
+    "mk_session_remote_done": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_int32]),
+    "mk_session_port_put": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_int32]),
+    "mk_session_stack_push": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_int32]),
+    "mk_session_stack_pop": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.POINTER(C.c_int32)]),
+    "mk_net_node_index": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mk_trace_lane": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.POINTER(mk_opts), C.c_void_p, C.c_uint32,
                                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]),
     "mk_version": (C.c_char_p, []),

@@ -221,6 +221,7 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
                 case OP_JGZ: if (acc[n] > 0) jump(I.arg); else retire(); break;
                 case OP_JLZ: if (acc[n] < 0) jump(I.arg); else retire(); break;
                 case OP_STUCK: break;
+                case OP_XSEND: case OP_XPUSH: case OP_XPOP: break; // no peers in a batch lane: blocks
                 case OP_IN:
                     if (in_avail) { // <-m.inChan (master.go:235)
                         in_avail = false;
@@ -827,6 +828,15 @@ struct SessParams {
     int32_t *in_val, *out_val; // [n]
     int32_t *sdepth;    // [nstack][n]
     int32_t *stk;       // [nstack][stack_cap][n]
+    // remote peers (MK_NODE_REMOTE_*, row f4): per program node, the state of
+    // its request to a peer (0 none, 1 asked, 2 answered by the host) and the
+    // value (sent, pushed, or popped); a call parked on them resumes
+    uint32_t *xst;      // [nprog][n]
+    int32_t *xval;      // [nprog][n]
+    int32_t *pin;       // [n] input of the current call not yet deposited
+    uint32_t *csteps;   // [n] steps retired by the current call so far
+    uint32_t mixed;     // network has remote peers: a round without change parks the call
+    uint32_t resume;    // continue each session's parked call (in ignored)
 };
 
 template <int NMAX>
@@ -842,7 +852,8 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     const bool live = gid < n;
 
     int64_t acc[NMAX], bak[NMAX];
-    int32_t ip[NMAX], pendv[NMAX];
+    int32_t ip[NMAX], pendv[NMAX], xval[NMAX];
+    uint32_t xst[NMAX];
     uint64_t pfull = 0;
     uint32_t pend = 0, hung = 0, io = 0;
     int32_t in_val = 0, out_val = 0;
@@ -853,6 +864,8 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
         bak[k] = on ? p.bak[(uint64_t)k * n + gid] : 0;
         ip[k] = on ? p.ip[(uint64_t)k * n + gid] : 0;
         pendv[k] = on ? p.pendv[(uint64_t)k * n + gid] : 0;
+        xst[k] = on && p.mixed ? p.xst[(uint64_t)k * n + gid] : 0u;
+        xval[k] = on && p.mixed ? p.xval[(uint64_t)k * n + gid] : 0;
     }
     if (live) {
         for (int q = 0; q < p.nprog * 4; ++q) port[q * B + tid] = p.port[(uint64_t)q * n + gid];
@@ -871,10 +884,14 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     // from one to the next (a burst of requests on one instance, one launch)
     for (uint32_t call = 0; call < p.ncalls; ++call) {
     const uint64_t ci = (uint64_t)call * n + gid;
-    const int32_t x = live ? (int32_t)p.in[ci] : 0; // int32(v) at GetInput (master.go:237)
-    bool active = live && dead == 0, deposited = false, got = false;
+    // a parked call (mixed networks) resumes with its input (deposited or not) and step count
+    const bool resumed = p.resume && live && ((io >> 3) & 1u);
+    const int32_t x = !live ? 0 : resumed ? p.pin[gid] : (int32_t)p.in[ci]; // int32(v) at GetInput (master.go:237)
+    bool active = live && dead == 0 && (!p.resume || resumed), got = false;
+    bool deposited = resumed && !((io >> 2) & 1u);
     int32_t result = 0;
-    uint32_t steps = 0;
+    uint32_t steps = resumed ? p.csteps[gid] : 0u;
+    bool parked = false;
 
     for (;;) {
         if (active) {
@@ -930,6 +947,16 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
                 case OP_JGZ: if (acc[k] > 0) jump(I.arg); else retire(); break;
                 case OP_JLZ: if (acc[k] < 0) jump(I.arg); else retire(); break;
                 case OP_STUCK: break;
+                case OP_XPOP: // popValue on a remote stack (program.go:524-536): the host makes the RPC
+                    if (xst[k] == 2u) {
+                        if (I.dst) acc[k] = xval[k];
+                        xst[k] = 0u;
+                        retire();
+                    } else if (xst[k] == 0u) {
+                        xst[k] = 1u;
+                        changed = true;
+                    }
+                    break;
                 case OP_IN:
                     if (in_full) { // <-m.inChan (master.go:235)
                         in_full = false;
@@ -1014,6 +1041,19 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
                     }
                     case OP_HANG: hung |= 1u << k; changed = true; break;
                     case OP_RETRY: if (consumed) changed = true; break;
+                    case OP_XSEND: case OP_XPUSH: // sendValue / pushValue to a peer (program.go:475-521)
+                        if (xst[k] == 2u) { // the host's RPC returned
+                            xst[k] = 0u;
+                            pend &= ~(1u << k);
+                            retire();
+                        } else if (xst[k] == 0u) { // source fetched once, held as the pending value
+                            pend |= 1u << k;
+                            pendv[k] = (int32_t)v;
+                            xval[k] = (int32_t)v; // int32(v) on the wire (program.go:498,516)
+                            xst[k] = 1u;
+                            changed = true;
+                        }
+                        break;
                     default: break;
                     }
                     break;
@@ -1026,15 +1066,22 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
                 dead = MK_ST_STACK_OVERFLOW;
                 active = false;
             } else if (!changed) {
-                dead = MK_ST_QUIESCENT;
+                if (p.mixed) parked = true; // waits on peers or on the host's inbound RPCs
+                else dead = MK_ST_QUIESCENT;
                 active = false;
             }
         }
     }
     if (live) {
         p.out[ci] = got ? result : 0;
-        p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : dead);
+        p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : parked ? MK_ST_REMOTE_WAIT : dead);
         if (p.steps) p.steps[ci] = steps;
+        // the call stays open while parked: input not yet deposited (bit 2), call open (bit 3)
+        io = (io & ~0xCu) | (parked && !deposited ? 4u : 0u) | (parked ? 8u : 0u);
+        if (parked) {
+            p.pin[gid] = x;
+            p.csteps[gid] = steps;
+        }
     }
     } // calls
 
@@ -1047,11 +1094,19 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
         p.ip[(uint64_t)k * n + gid] = ip[k];
         p.pendv[(uint64_t)k * n + gid] = pendv[k];
     }
+    if (p.mixed) {
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) {
+            if (k >= p.nprog) continue;
+            p.xst[(uint64_t)k * n + gid] = xst[k];
+            p.xval[(uint64_t)k * n + gid] = xval[k];
+        }
+    }
     for (int q = 0; q < p.nprog * 4; ++q) p.port[(uint64_t)q * n + gid] = port[q * B + tid];
     for (int q = 0; q < p.nstack; ++q) p.sdepth[(uint64_t)q * n + gid] = sdepth[q * B + tid];
     p.pfull[gid] = pfull;
     p.bits[gid] = (pend & 0xffffu) | (hung << 16);
-    p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (dead << 4);
+    p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (io & 0xCu) | (dead << 4);
     p.in_val[gid] = in_val;
     p.out_val[gid] = out_val;
 }
@@ -1811,11 +1866,12 @@ namespace mk {
 namespace {
 
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
-                   hipStream_t stream, uint32_t ncalls = 1)
+                   hipStream_t stream, uint32_t ncalls = 1, bool resume = false)
 {
     if (s->n == 0 || ncalls == 0) return MK_OK;
     SessParams p = s->p;
     p.ncalls = ncalls;
+    p.resume = resume ? 1u : 0u;
     p.in = d_in;
     p.out = d_out;
     p.status = d_status;
@@ -1992,7 +2048,8 @@ int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_s
     const size_t N = n ? n : 1, P = (size_t)s->nprog, S = (size_t)s->nstack;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t sz[] = {al(P * N * 8), al(P * N * 8), al(P * N * 4), al(P * N * 4), al(P * 4 * N * 4), al(N * 8),
-                         al(N * 4),     al(N * 4),     al(N * 4),     al(N * 4),     al(S * N * 4),     al(S * cap * N * 4)};
+                         al(N * 4),     al(N * 4),     al(N * 4),     al(N * 4),     al(S * N * 4),     al(S * cap * N * 4),
+                         al(P * N * 4), al(P * N * 4), al(N * 4),     al(N * 4)};
     size_t total = 0;
     for (size_t b : sz) total += b;
     if (hipMalloc(&s->d_state, total) != hipSuccess) return MK_ENOMEM;
@@ -2022,6 +2079,11 @@ int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_s
     p.out_val = (int32_t *)take(9);
     p.sdepth = (int32_t *)take(10);
     p.stk = (int32_t *)take(11);
+    p.xst = (uint32_t *)take(12);
+    p.xval = (int32_t *)take(13);
+    p.pin = (int32_t *)take(14);
+    p.csteps = (uint32_t *)take(15);
+    p.mixed = h->net.uses_remote ? 1u : 0u;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return MK_EDEVICE;
     if (hipMemsetAsync(s->d_state, 0, total, s->stream) != hipSuccess) return MK_EDEVICE; // post-/reset state
     if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
@@ -2059,10 +2121,38 @@ int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out
     return MK_OK;
 }
 
+extern "C++" {
+namespace mk {
+namespace {
+int session_host_calls(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
+                       uint32_t *steps, bool resume);
+}
+} // namespace mk
+}
+
 int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
                            uint32_t *steps)
 {
     if (!s || (s->n && ncalls && (!in || !out || !status))) return MK_EINVAL;
+    return mk::session_host_calls(s, in, ncalls, out, status, steps, false);
+}
+
+int mk_session_step(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps)
+{
+    if (!s || (s->n && (!out || !status))) return MK_EINVAL;
+    if (!in) { // resume: the kernel ignores the inputs
+        std::vector<int64_t> z(s->n ? s->n : 1, 0);
+        return mk::session_host_calls(s, z.data(), 1, out, status, steps, true);
+    }
+    return mk::session_host_calls(s, in, 1, out, status, steps, false);
+}
+
+extern "C++" {
+namespace mk {
+namespace {
+int session_host_calls(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
+                       uint32_t *steps, bool resume)
+{
     if (s->n == 0 || ncalls == 0) return MK_OK;
     if (ncalls > 0xffffffffull) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
@@ -2088,7 +2178,7 @@ int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int3
     uint8_t *dst = (uint8_t *)(b + a8 + a4 + a4);
     memcpy(hb, in, m * 8);
     if (hipMemcpyAsync(din, hb, m * 8, hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
-    int rc = mk::session_launch(s, din, dout, dst, steps ? dsteps : nullptr, s->stream, (uint32_t)ncalls);
+    int rc = mk::session_launch(s, din, dout, dst, steps ? dsteps : nullptr, s->stream, (uint32_t)ncalls, resume);
     if (rc) return rc;
     if (hipMemcpyAsync(hb + a8, dout, m * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
         hipMemcpyAsync(hb + a8 + a4 + a4, dst, m, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
@@ -2102,9 +2192,124 @@ int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int3
     return MK_OK;
 }
 
+// One element of session state (device), read or written synchronously on
+// the session's stream (ordered after its launches).  Caller holds s->mu.
+template <class T>
+int sget(mk_session *s, const T *dev, T &v)
+{
+    if (hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, s->stream) != hipSuccess) return MK_EDEVICE;
+    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+template <class T>
+int sput(mk_session *s, T *dev, const T &v)
+{
+    if (hipMemcpyAsync(dev, &v, sizeof(T), hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
+    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+} // namespace
+} // namespace mk
+}
+
 int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps)
 {
     return mk_session_compute_seq(s, in, 1, out, status, steps);
+}
+
+int mk_session_remote_poll(mk_session *s, size_t inst, mk_remote_req *reqs, int max, int *count)
+{
+    if (!s || !count || inst >= s->n || (max > 0 && !reqs)) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    *count = 0;
+    if (!s->p.mixed) return MK_OK;
+    const uint64_t n = s->n;
+    for (int k = 0; k < s->nprog; k++) {
+        uint32_t st = 0;
+        int rc = mk::sget(s, s->p.xst + (uint64_t)k * n + inst, st);
+        if (rc) return rc;
+        if (st != 1u) continue;
+        int32_t ip = 0, val = 0;
+        if ((rc = mk::sget(s, s->p.ip + (uint64_t)k * n + inst, ip)) ||
+            (rc = mk::sget(s, s->p.xval + (uint64_t)k * n + inst, val)))
+            return rc;
+        const mk::Insn &I = s->h->net.code[s->h->net.base[k] + (uint32_t)ip];
+        if (*count >= max) return MK_EINVAL;
+        mk_remote_req &r = reqs[(*count)++];
+        r.node = (uint32_t)k;
+        r.op = I.op == mk::OP_XSEND ? MK_REMOTE_SEND : I.op == mk::OP_XPUSH ? MK_REMOTE_PUSH : MK_REMOTE_POP;
+        r.remote = I.op == mk::OP_XSEND ? I.arg / 4u : I.arg;
+        r.reg = I.op == mk::OP_XSEND ? I.arg % 4u : 0u;
+        r.value = val;
+    }
+    return MK_OK;
+}
+
+int mk_session_remote_done(mk_session *s, size_t inst, uint32_t node, int32_t value)
+{
+    if (!s || inst >= s->n || node >= (uint32_t)s->nprog || !s->p.mixed) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    const uint64_t off = (uint64_t)node * s->n + inst;
+    uint32_t st = 0;
+    int rc = mk::sget(s, s->p.xst + off, st);
+    if (rc) return rc;
+    if (st != 1u) return MK_EINVAL; // no request outstanding
+    if ((rc = mk::sput(s, s->p.xval + off, value))) return rc;
+    return mk::sput(s, s->p.xst + off, (uint32_t)2u);
+}
+
+int mk_session_port_put(mk_session *s, size_t inst, uint32_t node, uint32_t reg, int32_t value)
+{
+    if (!s || inst >= s->n || node >= (uint32_t)s->nprog || reg > 3) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    const uint32_t q = node * 4 + reg;
+    uint64_t full = 0;
+    int rc = mk::sget(s, s->p.pfull + inst, full);
+    if (rc) return rc;
+    if ((full >> q) & 1ull) return MK_EBUSY; // p.rK <- v blocks while full (program.go:163)
+    if ((rc = mk::sput(s, s->p.port + (uint64_t)q * s->n + inst, value))) return rc;
+    return mk::sput(s, s->p.pfull + inst, (uint64_t)(full | (1ull << q)));
+}
+
+int mk_session_stack_push(mk_session *s, size_t inst, uint32_t stack, int32_t value)
+{
+    if (!s || inst >= s->n || stack >= (uint32_t)s->nstack) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    int32_t d = 0;
+    int rc = mk::sget(s, s->p.sdepth + (uint64_t)stack * s->n + inst, d);
+    if (rc) return rc;
+    if ((uint32_t)d >= s->cap) return MK_ELIMIT; // stack_cap (the reference's stacks are unbounded)
+    if ((rc = mk::sput(s, s->p.stk + ((uint64_t)stack * s->cap + (uint32_t)d) * s->n + inst, value))) return rc;
+    return mk::sput(s, s->p.sdepth + (uint64_t)stack * s->n + inst, (int32_t)(d + 1));
+}
+
+int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *value)
+{
+    if (!s || !value || inst >= s->n || stack >= (uint32_t)s->nstack) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    int32_t d = 0;
+    int rc = mk::sget(s, s->p.sdepth + (uint64_t)stack * s->n + inst, d);
+    if (rc) return rc;
+    if (d <= 0) return MK_EBUSY; // waitPop blocks while empty (stack.go:133-155)
+    if ((rc = mk::sget(s, s->p.stk + ((uint64_t)stack * s->cap + (uint32_t)(d - 1)) * s->n + inst, *value)))
+        return rc;
+    return mk::sput(s, s->p.sdepth + (uint64_t)stack * s->n + inst, (int32_t)(d - 1));
+}
+
+int mk_net_node_index(const mk_net *h, const char *name, int *kind, int *index)
+{
+    if (!h || !name || !kind || !index) return MK_EINVAL;
+    const mk::Network &N = h->net;
+    for (int i = 0; i < N.nprog; i++)
+        if (N.prog_names[i] == name) { *kind = MK_NODE_PROGRAM; *index = i; return MK_OK; }
+    for (int i = 0; i < N.nstack; i++)
+        if (N.stack_names[i] == name) { *kind = MK_NODE_STACK; *index = i; return MK_OK; }
+    for (size_t i = 0; i < N.remote_names.size(); i++)
+        if (N.remote_names[i] == name) { *kind = N.remote_kinds[i]; *index = (int)i; return MK_OK; }
+    return MK_EINVAL;
 }
 
 void mk_session_free(mk_session *s) { delete s; }

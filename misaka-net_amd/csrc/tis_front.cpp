@@ -321,6 +321,8 @@ struct Resolver {
             if (net.stack_names[i] == name) { idx = i; return NK_STACK; }
         for (auto &n : nodes)
             if (n.kind == NK_MASTER && n.name == name) { idx = 0; return NK_MASTER; }
+        for (size_t i = 0; i < net.remote_names.size(); i++)
+            if (net.remote_names[i] == name) { idx = (int)i; return net.remote_kinds[i]; }
         return -1;
     }
 };
@@ -353,6 +355,7 @@ Insn failing_network_op(int kind, uint8_t src, int64_t imm)
 int lower_network(const std::vector<NodeSpec> &nodes, Network &net, std::string &err)
 {
     net = Network();
+    if (nodes.size() > 4096) { err = "too many nodes"; return MK_ELIMIT; }
     std::vector<const NodeSpec *> progs, stacks;
     int nmaster = 0;
     for (size_t i = 0; i < nodes.size(); i++) {
@@ -362,6 +365,10 @@ int lower_network(const std::vector<NodeSpec> &nodes, Network &net, std::string 
         case NK_PROGRAM: progs.push_back(&nodes[i]); break;
         case NK_STACK: stacks.push_back(&nodes[i]); break;
         case NK_MASTER: nmaster++; break;
+        case NK_REMOTE_PROGRAM: case NK_REMOTE_STACK:
+            net.remote_names.push_back(nodes[i].name);
+            net.remote_kinds.push_back(nodes[i].kind);
+            break;
         default: err = "invalid node type"; return MK_EINVAL; // master.go:437
         }
     }
@@ -426,6 +433,9 @@ int lower_network(const std::vector<NodeSpec> &nodes, Network &net, std::string 
                 int kind = R.find(host, idx);
                 if (kind == NK_PROGRAM) {
                     in.op = OP_SEND; in.src = s; in.imm = v; in.arg = (uint16_t)(idx * 4 + k);
+                } else if (kind == NK_REMOTE_PROGRAM) {
+                    in.op = OP_XSEND; in.src = s; in.imm = v; in.arg = (uint16_t)(idx * 4 + k);
+                    net.uses_remote = true;
                 } else {
                     in = failing_network_op(kind, s, v);
                 }
@@ -447,6 +457,9 @@ int lower_network(const std::vector<NodeSpec> &nodes, Network &net, std::string 
                 if (kind == NK_STACK) {
                     in.op = OP_PUSH; in.src = s; in.imm = v; in.arg = (uint16_t)idx;
                     net.uses_stacks = true;
+                } else if (kind == NK_REMOTE_STACK) {
+                    in.op = OP_XPUSH; in.src = s; in.imm = v; in.arg = (uint16_t)idx;
+                    net.uses_remote = true;
                 } else {
                     in = failing_network_op(kind, s, v);
                 }
@@ -457,6 +470,9 @@ int lower_network(const std::vector<NodeSpec> &nodes, Network &net, std::string 
                 if (kind == NK_STACK) {
                     in.op = OP_POP; in.arg = (uint16_t)idx; in.dst = L.b == "ACC";
                     net.uses_stacks = true;
+                } else if (kind == NK_REMOTE_STACK) {
+                    in.op = OP_XPOP; in.arg = (uint16_t)idx; in.dst = L.b == "ACC";
+                    net.uses_remote = true;
                 } else {
                     in = failing_network_op(kind, SRC_NIL, 0);
                 }
@@ -477,7 +493,8 @@ std::string disasm(const Network &net)
 {
     static const char *ops[OP_COUNT] = {"NOP", "SWP", "SAV", "NEG", "MOV", "ADD", "SUB",
                                         "JMP", "JEZ", "JNZ", "JGZ", "JLZ", "JRO", "SEND",
-                                        "PUSH", "POP", "IN", "OUT", "STUCK", "HANG", "RETRY"};
+                                        "PUSH", "POP", "IN", "OUT", "STUCK", "HANG", "RETRY",
+                                        "XSEND", "XPUSH", "XPOP"};
     static const char *srcs[] = {"IMM", "ACC", "NIL", "R0", "R1", "R2", "R3"};
     std::string s;
     char buf[160];

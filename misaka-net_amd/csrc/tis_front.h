@@ -33,6 +33,13 @@ enum Op : uint8_t {
     OP_STUCK, // never completes, no side effect (Atoi range error; RPC to a wrong service without a consumed source)
     OP_HANG,  // acquire src, then hang forever (grpc.Dial WithBlock to an unknown host)
     OP_RETRY, // acquire src (consumes Rk), never retires (Unimplemented RPC retried forever)
+    // Network ops to peers outside this executor (MK_NODE_REMOTE_*, row f4):
+    // a stateful session hands them to the host, which makes the RPC
+    // (Program.Send / Stack.Push / Stack.Pop); batch lanes have no peers and
+    // block on them.
+    OP_XSEND, // remote port[arg] <- int32(src) (arg = remote * 4 + k)   MOV_*_NETWORK
+    OP_XPUSH, // remote stack[arg].push(int32(src))                      PUSH_*
+    OP_XPOP,  // ACC|NIL <- remote stack[arg].pop()                      POP
     OP_COUNT
 };
 
@@ -81,7 +88,7 @@ bool parse_program(const std::string &src, Program &out, std::string &err);
 // strconv.Atoi on a `-?\d+` token (64-bit int).  false on range error.
 bool atoi64(const std::string &tok, int64_t &v);
 
-enum NodeKind { NK_PROGRAM = 0, NK_STACK = 1, NK_MASTER = 2 };
+enum NodeKind { NK_PROGRAM = 0, NK_STACK = 1, NK_MASTER = 2, NK_REMOTE_PROGRAM = 3, NK_REMOTE_STACK = 4 };
 
 struct NodeSpec {
     std::string name;
@@ -97,6 +104,11 @@ struct Network {
     std::vector<Insn> code;
     std::vector<uint32_t> base, len; // per program node
     bool uses_stacks = false;
+    // peers served elsewhere (MK_NODE_REMOTE_*), in declaration order; the
+    // X-ops' remote index is into this list
+    std::vector<std::string> remote_names;
+    std::vector<int> remote_kinds; // NK_REMOTE_PROGRAM / NK_REMOTE_STACK
+    bool uses_remote = false;
 };
 
 // Returns 0 or an MK_E* code with err filled.

@@ -974,6 +974,10 @@ bool Compiler::run(SchedProgram &out, std::string &why)
 bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
                       SchedProgram &out, std::string &why)
 {
+    if (net.uses_remote) { // X-ops wait on the host: only the interpreters run them
+        why = "network addresses remote peers (MK_NODE_REMOTE_*)";
+        return false;
+    }
     Compiler c(net, stack_cap, stop_on_output, lim);
     return c.run(out, why);
 }

@@ -43,11 +43,12 @@ def tokenize(program: str) -> list[list[str]]:
 @dataclass
 class NodeSpec:
     name: str
-    kind: str = "program"  # "program" | "stack" | "master"
+    kind: str = "program"  # "program" | "stack" | "master" | "remote_program" | "remote_stack"
     program: str = ""
 
 
-_KINDS = {"program": N.MK_NODE_PROGRAM, "stack": N.MK_NODE_STACK, "master": N.MK_NODE_MASTER}
+_KINDS = {"program": N.MK_NODE_PROGRAM, "stack": N.MK_NODE_STACK, "master": N.MK_NODE_MASTER,
+          "remote_program": N.MK_NODE_REMOTE_PROGRAM, "remote_stack": N.MK_NODE_REMOTE_STACK}
 
 
 @dataclass
