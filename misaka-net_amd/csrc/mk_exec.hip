@@ -178,148 +178,142 @@ __global__ void __launch_bounds__(kBlock) tis_exec(const Insn *__restrict__ code
         for (int n = 0; n < NMAX; ++n) {
             if (n >= p.nprog) continue; // wave-uniform; keeps the loop fully unrollable
             const uint32_t len = p.len[n];
-            bool pending = active && !done && !((hung >> n) & 1u);
-            unsigned long long todo = __ballot(pending);
-            while (todo) {
-                const int lead = __builtin_ctzll(todo);
-                const int u = __builtin_amdgcn_readlane(ip[n], lead);
-                const bool mine = pending && ip[n] == u;
-                todo &= ~__ballot(mine);
-                const Insn I = fetch(code, p.base[n] + (uint32_t)u); // one s_load_dwordx4
-                if (!mine) continue;
-                pending = false;
-                auto record = [&]() { // mk_trace_lane: one entry per retired instruction of input 0
-                    if (p.trace && idx == 0 && ntrace < p.trace_max) {
-                        mk_trace_entry &e = p.trace[ntrace++];
-                        e.round = round;
-                        e.node = (uint16_t)n;
-                        e.ip = (uint16_t)u;
-                        e.acc = acc[n];
-                        e.bak = bak[n];
-                    }
-                };
-                auto retire = [&]() {
-                    ip[n] = (ip[n] + 1 == (int32_t)len) ? 0 : ip[n] + 1; // program.go:429
-                    ++steps;
-                    changed = true;
-                    record();
-                };
-                auto jump = [&](int32_t t) {
-                    ip[n] = t;
-                    ++steps;
-                    changed = true;
-                    record();
-                };
-                switch (I.op) {
-                case OP_NOP: retire(); break;
-                case OP_SWP: { const int64_t t = acc[n]; acc[n] = bak[n]; bak[n] = t; retire(); break; }
-                case OP_SAV: bak[n] = acc[n]; retire(); break;
-                case OP_NEG: acc[n] = (int64_t)(0ull - (uint64_t)acc[n]); retire(); break;
-                case OP_JMP: jump(I.arg); break;
-                case OP_JEZ: if (acc[n] == 0) jump(I.arg); else retire(); break;
-                case OP_JNZ: if (acc[n] != 0) jump(I.arg); else retire(); break;
-                case OP_JGZ: if (acc[n] > 0) jump(I.arg); else retire(); break;
-                case OP_JLZ: if (acc[n] < 0) jump(I.arg); else retire(); break;
-                case OP_STUCK: break;
-                case OP_XSEND: case OP_XPUSH: case OP_XPOP: break; // no peers in a batch lane: blocks
-                case OP_IN:
-                    if (in_avail) { // <-m.inChan (master.go:235)
-                        in_avail = false;
-                        if (I.dst) acc[n] = in_val;
-                        retire();
-                    }
-                    break;
-                case OP_POP: {
-                    int32_t *dp = &sdepth[I.arg * B + tid];
-                    const int32_t d = *dp;
-                    if (d > 0) { // waitPop blocks while empty (stack.go:133-155)
-                        const uint32_t e = (uint32_t)d - 1;
-                        int32_t *rp = &ring[((uint32_t)I.arg * W + (e & (W - 1))) * B + tid];
-                        const int32_t v = *rp;
-                        if (e >= W)
-                            *rp = p.spill[((uint64_t)I.arg * p.spill_rows + (e - W)) * p.lanes + gid];
-                        *dp = (int32_t)e;
-                        if (I.dst) acc[n] = v;
-                        retire();
-                    }
-                    break;
+            const bool pending = active && !done && !((hung >> n) & 1u);
+            if (!__ballot(pending)) continue;
+            // Every lane fetches its own instruction (a 16-byte vector load of
+            // hot, cache-resident code) and the op bodies below are masked
+            // regions: lanes at different instructions run in ONE pass, a
+            // region costs only when some lane needs it.  (The scalar-fetch
+            // waterfall this replaces made one serial pass per distinct ip.)
+            const int u = ip[n];
+            uint4 w = make_uint4(0u, 0u, 0u, 0u);
+            if (pending) w = reinterpret_cast<const uint4 *>(code)[p.base[n] + (uint32_t)u];
+            const uint32_t op = pending ? (w.x & 0xffu) : (uint32_t)OP_STUCK;
+            const uint32_t src = (w.x >> 8) & 0xffu;
+            const bool dacc = ((w.x >> 16) & 0xffu) != 0u;
+            const uint32_t arg = w.y & 0xffffu;
+            const int64_t imm = (int64_t)(((uint64_t)w.w << 32) | (uint64_t)w.z);
+            bool ret = false;             // retires: ip advances (or jumps), steps++
+            int32_t tgt = -1;             // jump target when >= 0
+            auto record = [&]() { // mk_trace_lane: one entry per retired instruction of input 0
+                if (p.trace && idx == 0 && ntrace < p.trace_max) {
+                    mk_trace_entry &e = p.trace[ntrace++];
+                    e.round = round;
+                    e.node = (uint16_t)n;
+                    e.ip = (uint16_t)u;
+                    e.acc = acc[n];
+                    e.bak = bak[n];
                 }
-                default: {
-                    // Ops with a source operand: getFromSrc (program.go:434-472).
-                    const bool pn = (pend >> n) & 1u;
-                    int64_t v = 0;
-                    bool consumed = false;
-                    if (pn) {
-                        v = pendv[n];
-                    } else if (I.src == SRC_IMM) {
-                        v = I.imm;
-                    } else if (I.src == SRC_ACC) {
-                        v = acc[n];
-                    } else if (I.src >= SRC_R0) {
-                        const uint32_t slot = (uint32_t)n * 4 + (I.src - SRC_R0);
-                        if (!((pfull >> slot) & 1ull)) break; // receive blocks
+            };
+            // ops without a source operand
+            if (op == OP_NOP) ret = true;
+            if (op == OP_SWP) { const int64_t t = acc[n]; acc[n] = bak[n]; bak[n] = t; ret = true; }
+            if (op == OP_SAV) { bak[n] = acc[n]; ret = true; }
+            if (op == OP_NEG) { acc[n] = (int64_t)(0ull - (uint64_t)acc[n]); ret = true; }
+            if (op >= OP_JMP && op <= OP_JLZ) {
+                const int64_t a = acc[n];
+                const bool take = op == OP_JMP || (op == OP_JEZ && a == 0) || (op == OP_JNZ && a != 0) ||
+                                  (op == OP_JGZ && a > 0) || (op == OP_JLZ && a < 0);
+                ret = true;
+                tgt = take ? (int32_t)arg : -1;
+            }
+            if (op == OP_IN && in_avail) { // <-m.inChan (master.go:235)
+                in_avail = false;
+                if (dacc) acc[n] = in_val;
+                ret = true;
+            }
+            if (op == OP_POP) {
+                int32_t *dp = &sdepth[arg * B + tid];
+                const int32_t d = *dp;
+                if (d > 0) { // waitPop blocks while empty (stack.go:133-155)
+                    const uint32_t e = (uint32_t)d - 1;
+                    int32_t *rp = &ring[(arg * W + (e & (W - 1))) * B + tid];
+                    const int32_t v = *rp;
+                    if (e >= W) *rp = p.spill[((uint64_t)arg * p.spill_rows + (e - W)) * p.lanes + gid];
+                    *dp = (int32_t)e;
+                    if (dacc) acc[n] = v;
+                    ret = true;
+                }
+            }
+            // ops with a source operand: getFromSrc (program.go:434-472)
+            const bool srcop = op == OP_MOV || op == OP_ADD || op == OP_SUB || op == OP_JRO || op == OP_SEND ||
+                               op == OP_OUT || op == OP_PUSH || op == OP_HANG || op == OP_RETRY;
+            const bool pn = (pend >> n) & 1u;
+            bool have = srcop, consumed = false;
+            int64_t v = 0;
+            if (srcop) {
+                if (pn) v = pendv[n];
+                else if (src == SRC_IMM) v = imm;
+                else if (src == SRC_ACC) v = acc[n];
+                else if (src >= SRC_R0) {
+                    const uint32_t slot = (uint32_t)n * 4 + (src - SRC_R0);
+                    if ((pfull >> slot) & 1ull) {
                         v = port[slot * B + tid];
                         pfull &= ~(1ull << slot);
                         consumed = true;
+                    } else {
+                        have = false; // receive blocks
                     }
-                    switch (I.op) {
-                    case OP_MOV: if (I.dst) acc[n] = v; retire(); break;
-                    case OP_ADD: acc[n] = (int64_t)((uint64_t)acc[n] + (uint64_t)v); retire(); break;
-                    case OP_SUB: acc[n] = (int64_t)((uint64_t)acc[n] - (uint64_t)v); retire(); break;
-                    case OP_JRO: {
-                        // IntClamp(ptr+v, 0, len-1), int64 wrapping add (program.go:354,362)
-                        int64_t t = (int64_t)((uint64_t)(int64_t)ip[n] + (uint64_t)v);
-                        t = t > (int64_t)len - 1 ? (int64_t)len - 1 : t;
-                        t = t < 0 ? 0 : t;
-                        jump((int32_t)t);
-                        break;
+                }
+            }
+            if (have) {
+                if (op == OP_MOV) { if (dacc) acc[n] = v; ret = true; }
+                if (op == OP_ADD) { acc[n] = (int64_t)((uint64_t)acc[n] + (uint64_t)v); ret = true; }
+                if (op == OP_SUB) { acc[n] = (int64_t)((uint64_t)acc[n] - (uint64_t)v); ret = true; }
+                if (op == OP_JRO) { // IntClamp(ptr+v, 0, len-1), int64 wrapping add (program.go:354,362)
+                    int64_t t = (int64_t)((uint64_t)(int64_t)u + (uint64_t)v);
+                    t = t > (int64_t)len - 1 ? (int64_t)len - 1 : t;
+                    t = t < 0 ? 0 : t;
+                    ret = true;
+                    tgt = (int32_t)t;
+                }
+                if (op == OP_SEND) {
+                    if (!((pfull >> arg) & 1ull)) { // p.rK <- int32(v) (program.go:163,498)
+                        port[arg * B + tid] = (int32_t)v;
+                        pfull |= 1ull << arg;
+                        pend &= ~(1u << n);
+                        ret = true;
+                    } else if (!pn) {
+                        pend |= 1u << n;
+                        pendv[n] = (int32_t)v;
+                        changed = true;
                     }
-                    case OP_SEND: {
-                        const uint32_t slot = I.arg;
-                        if (!((pfull >> slot) & 1ull)) { // p.rK <- int32(v) (program.go:163,498)
-                            port[slot * B + tid] = (int32_t)v;
-                            pfull |= 1ull << slot;
-                            pend &= ~(1u << n);
-                            retire();
-                        } else if (!pn) {
-                            pend |= 1u << n;
-                            pendv[n] = (int32_t)v;
-                            changed = true;
-                        }
-                        break;
+                }
+                if (op == OP_OUT) {
+                    if (out_cnt < 2) { // outChan cap 1 + one /compute read (master.go:219,246)
+                        if (out_cnt == 0) out_val = (int32_t)v;
+                        ++out_cnt;
+                        pend &= ~(1u << n);
+                        ret = true;
+                        if (p.flags & MK_FLAG_STOP_ON_OUTPUT) { done = true; reason = MK_ST_OUTPUT_STOP; }
+                    } else if (!pn) {
+                        pend |= 1u << n;
+                        pendv[n] = (int32_t)v;
+                        changed = true;
                     }
-                    case OP_OUT:
-                        if (out_cnt < 2) { // outChan cap 1 + one /compute read (master.go:219,246)
-                            if (out_cnt == 0) out_val = (int32_t)v;
-                            ++out_cnt;
-                            pend &= ~(1u << n);
-                            retire();
-                            if (p.flags & MK_FLAG_STOP_ON_OUTPUT) { done = true; reason = MK_ST_OUTPUT_STOP; }
-                        } else if (!pn) {
-                            pend |= 1u << n;
-                            pendv[n] = (int32_t)v;
-                            changed = true;
-                        }
-                        break;
-                    case OP_PUSH: {
-                        int32_t *dp = &sdepth[I.arg * B + tid];
-                        const uint32_t d = (uint32_t)*dp;
-                        if (d >= p.stack_cap) { done = true; reason = MK_ST_STACK_OVERFLOW; break; }
-                        int32_t *rp = &ring[((uint32_t)I.arg * W + (d & (W - 1))) * B + tid];
-                        if (d >= W)
-                            p.spill[((uint64_t)I.arg * p.spill_rows + (d - W)) * p.lanes + gid] = *rp;
+                }
+                if (op == OP_PUSH) {
+                    int32_t *dp = &sdepth[arg * B + tid];
+                    const uint32_t d = (uint32_t)*dp;
+                    if (d >= p.stack_cap) {
+                        done = true;
+                        reason = MK_ST_STACK_OVERFLOW;
+                    } else {
+                        int32_t *rp = &ring[(arg * W + (d & (W - 1))) * B + tid];
+                        if (d >= W) p.spill[((uint64_t)arg * p.spill_rows + (d - W)) * p.lanes + gid] = *rp;
                         *rp = (int32_t)v; // ValueMessage{int32(v)} (program.go:516)
                         *dp = (int32_t)(d + 1);
-                        retire();
-                        break;
+                        ret = true;
                     }
-                    case OP_HANG: hung |= 1u << n; changed = true; break;
-                    case OP_RETRY: if (consumed) changed = true; break;
-                    default: break;
-                    }
-                    break;
                 }
-                }
+                if (op == OP_HANG) { hung |= 1u << n; changed = true; }
+                if (op == OP_RETRY && consumed) changed = true;
+            }
+            if (ret) {
+                ip[n] = tgt >= 0 ? tgt : ((u + 1 == (int32_t)len) ? 0 : u + 1); // program.go:429
+                ++steps;
+                changed = true;
+                record();
             }
         }
         if (active && !done) {
@@ -2041,7 +2035,8 @@ int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_s
         int rc = mk::ensure_device(h, device);
         if (rc) return rc;
         s->nprog = h->net.nprog;
-        s->nstack = h->net.uses_stacks ? h->net.nstack : 0;
+        // remote peers of a mixed deployment may push to / pop from local stacks
+        s->nstack = h->net.uses_stacks || h->net.uses_remote ? h->net.nstack : 0;
     }
     mk::DeviceGuard g(device);
     // one allocation, 256-byte aligned arrays, [field][session]

@@ -125,7 +125,8 @@ class MixedHost:
                     rc = N.lib().mk_session_port_put(self.sess._h, 0, node, reg, value)
                 if rc == N.MK_EBUSY:
                     raise _Busy()
-                N.check(rc, "mk_session_port_put")
+                if rc != N.MK_OK:
+                    context.abort(grpc.StatusCode.INTERNAL, f"{N.ERROR_NAMES.get(rc, rc)}: mk_session_port_put")
                 self._event()
                 return wire.EMPTY
 
@@ -141,7 +142,8 @@ class MixedHost:
                 rc = N.lib().mk_session_stack_push(self.sess._h, 0, idx, value)
             if rc == N.MK_ELIMIT:
                 context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, "stack_cap reached")
-            N.check(rc, "mk_session_stack_push")
+            if rc != N.MK_OK:
+                context.abort(grpc.StatusCode.INTERNAL, f"{N.ERROR_NAMES.get(rc, rc)}: mk_session_stack_push")
             self._event()
             return wire.EMPTY
 
@@ -157,7 +159,8 @@ class MixedHost:
                     rc = N.lib().mk_session_stack_pop(self.sess._h, 0, idx, C.byref(v))
                 if rc == N.MK_EBUSY:
                     raise _Busy()
-                N.check(rc, "mk_session_stack_pop")
+                if rc != N.MK_OK:
+                    context.abort(grpc.StatusCode.INTERNAL, f"{N.ERROR_NAMES.get(rc, rc)}: mk_session_stack_pop")
                 self._event()
                 return v.value
 

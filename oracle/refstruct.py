@@ -304,6 +304,7 @@ class ProgramNodeEmu:
             except (grpc.RpcError, ValueError):
                 if self.net.stop.is_set():
                     return
+                self.net.stop.wait(0.01)  # the reference retries at once; the emulation backs off
 
 
 class StackNodeEmu:
