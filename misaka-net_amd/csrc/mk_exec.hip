@@ -27,6 +27,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -1188,8 +1189,13 @@ struct DevCtx {
     int cus = 0;
     int32_t *d_spill = nullptr;
     size_t spill_bytes = 0;
-    void *d_stage = nullptr; // host-API staging buffer
-    size_t stage_bytes = 0;
+    // host-API staging (mk_compute_batch): two chunk buffers on the device
+    // and their pinned host mirrors, so a chunk's host copies overlap the
+    // previous chunk's transfers and launch
+    void *d_stage = nullptr;
+    void *h_stage = nullptr;
+    size_t stage_bytes = 0;        // per buffer
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
     unsigned long long *d_partials = nullptr; // per-wave counters
     size_t partials_bytes = 0;
     hipStream_t stream = nullptr;
@@ -1211,6 +1217,7 @@ struct mk_net {
     mk::DevCtx dev[mk::kMaxDevices];
     std::vector<std::unique_ptr<mk::SchedCache>> sched;
     mk::JitLimits jit_lim = mk::JitLimits::from_env(); // knob snapshot at load (tis_jit.h)
+    uint64_t host_chunk = 0;                           // mk_compute_batch chunk (inputs)
     ~mk_net()
     {
         int prev = 0;
@@ -1223,6 +1230,9 @@ struct mk_net {
             (void)hipFree(c.d_code);
             (void)hipFree(c.d_spill);
             (void)hipFree(c.d_stage);
+            (void)hipHostFree(c.h_stage);
+            for (hipEvent_t e : c.stage_ev)
+                if (e) (void)hipEventDestroy(e);
             (void)hipFree(c.d_partials);
             for (auto &sc : sched) {
                 (void)hipFree(sc->dev[d].d_code);
@@ -1627,6 +1637,15 @@ int ensure_jit_device(SchedCache *sc, int d)
     return MK_OK;
 }
 
+// Host-API chunk (inputs per pinned staging buffer, 4M); MK_HOST_CHUNK
+// overrides it for networks loaded afterwards (tests: many chunks per batch).
+uint64_t host_chunk_from_env()
+{
+    const char *e = std::getenv("MK_HOST_CHUNK");
+    const unsigned long long x = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    return x ? (uint64_t)x : (uint64_t)1 << 22;
+}
+
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
 int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, uint32_t flags,
@@ -1930,6 +1949,7 @@ int mk_net_load(const mk_node_desc *nodes, int n, mk_net **out, char *err, size_
         delete h;
         return rc;
     }
+    h->host_chunk = mk::host_chunk_from_env();
     mk::set_err(err, err_len, "");
     *out = h;
     return MK_OK;
@@ -1945,60 +1965,110 @@ int mk_compute_batch(mk_net *h, const int64_t *in, size_t n, int32_t *out, uint8
     std::lock_guard<std::mutex> lk(h->mu);
     const int ndev = mk::device_count();
     if (ndev <= 0) return MK_EDEVICE;
+    // device_mask: the GPUs this process shards the batch over (contiguous
+    // ranges); a bit naming a GPU that does not exist is an error
     std::vector<int> devs;
     const uint32_t mask = opts ? opts->device_mask : 0u;
     if (mask == 0) devs.push_back(0);
-    for (int d = 0; d < ndev && d < 32; d++)
-        if (mask & (1u << d)) devs.push_back(d);
-    if (devs.empty()) return MK_EINVAL;
+    for (int d = 0; d < 32; d++)
+        if (mask & (1u << d)) {
+            if (d >= ndev || d >= mk::kMaxDevices) return MK_EINVAL;
+            devs.push_back(d);
+        }
     const size_t G = devs.size();
-    struct Shard { int d; size_t lo, hi; int64_t *din; int32_t *dout; uint8_t *dst; uint32_t *dsteps; };
-    std::vector<Shard> sh;
+    // Each device's range goes through in chunks: host values are copied
+    // into pinned buffers (two per device, alternating), moved by DMA, run,
+    // and the results copied back out of pinned memory -- the host copies of
+    // one chunk overlap the transfers and launch of the other.
+    struct Job { int d; size_t lo, hi; };
+    std::vector<Job> jobs;
     for (size_t g = 0; g < G; g++) {
-        Shard s{devs[g], n * g / G, n * (g + 1) / G, nullptr, nullptr, nullptr, nullptr};
-        if (s.hi > s.lo) sh.push_back(s);
+        const size_t lo = n * g / G, hi = n * (g + 1) / G;
+        if (hi > lo) jobs.push_back({devs[g], lo, hi});
     }
-    for (auto &s : sh) {
-        int rc = mk::ensure_device(h, s.d);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t C = (size_t)std::min<uint64_t>(h->host_chunk, n);
+    const size_t a8 = al(C * 8), a4 = al(C * 4), a1 = al(C);
+    const size_t per = a8 + a4 + a4 + a1; // in, out, steps, status
+    for (auto &j : jobs) {
+        int rc = mk::ensure_device(h, j.d);
         if (rc) return rc;
-        mk::DevCtx &c = h->dev[s.d];
-        mk::DeviceGuard g(s.d);
-        const size_t m = s.hi - s.lo;
-        const size_t a8 = (m * 8 + 255) & ~(size_t)255, a4 = (m * 4 + 255) & ~(size_t)255,
-                     a1 = (m + 255) & ~(size_t)255;
-        const size_t need = a8 + a4 + a4 + a1;
-        if (need > c.stage_bytes) {
+        mk::DevCtx &c = h->dev[j.d];
+        mk::DeviceGuard g(j.d);
+        if (per > c.stage_bytes) {
             (void)hipStreamSynchronize(c.stream);
             (void)hipFree(c.d_stage);
-            c.d_stage = nullptr;
+            (void)hipHostFree(c.h_stage);
+            c.d_stage = c.h_stage = nullptr;
             c.stage_bytes = 0;
-            if (hipMalloc(&c.d_stage, need) != hipSuccess) return MK_ENOMEM;
-            c.stage_bytes = need;
+            if (hipMalloc(&c.d_stage, 2 * per) != hipSuccess) return MK_ENOMEM;
+            if (hipHostMalloc(&c.h_stage, 2 * per, hipHostMallocDefault) != hipSuccess) return MK_ENOMEM;
+            c.stage_bytes = per;
         }
-        char *base = (char *)c.d_stage;
-        s.din = (int64_t *)base;
-        s.dout = (int32_t *)(base + a8);
-        s.dsteps = (uint32_t *)(base + a8 + a4);
-        s.dst = (uint8_t *)(base + a8 + a4 + a4);
-        if (hipMemcpyAsync(s.din, in + s.lo, m * 8, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-            return MK_EDEVICE;
-        mk_input mi{};
-        mi.kind = MK_IN_I64;
-        mi.data = s.din;
-        rc = mk::launch_locked(h, s.d, &mi, m, s.dout, s.dst, steps ? s.dsteps : nullptr, nullptr, opts, c.stream);
-        if (rc) return rc;
-        if (hipMemcpyAsync(out + s.lo, s.dout, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
-            hipMemcpyAsync(status + s.lo, s.dst, m, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
-            return MK_EDEVICE;
-        if (steps && hipMemcpyAsync(steps + s.lo, s.dsteps, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
-            return MK_EDEVICE;
+        for (hipEvent_t &e : c.stage_ev)
+            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
     }
-    int rc = MK_OK;
-    for (auto &s : sh) {
-        mk::DeviceGuard g(s.d);
-        if (hipStreamSynchronize(h->dev[s.d].stream) != hipSuccess) rc = MK_EDEVICE;
+    // per device: chunk k uses buffer k & 1; before a buffer is refilled its
+    // previous chunk's results are copied out (after its event)
+    struct Pend { size_t lo = 0, m = 0; bool live = false; };
+    std::vector<std::array<Pend, 2>> pend(jobs.size());
+    auto drain = [&](size_t ji, int b) -> int {
+        Pend &q = pend[ji][b];
+        if (!q.live) return MK_OK;
+        mk::DevCtx &c = h->dev[jobs[ji].d];
+        if (hipEventSynchronize(c.stage_ev[b]) != hipSuccess) return MK_EDEVICE;
+        const char *hb = (const char *)c.h_stage + (size_t)b * c.stage_bytes;
+        memcpy(out + q.lo, hb + a8, q.m * 4);
+        if (steps) memcpy(steps + q.lo, hb + a8 + a4, q.m * 4);
+        memcpy(status + q.lo, hb + a8 + a4 + a4, q.m);
+        q.live = false;
+        return MK_OK;
+    };
+    std::vector<size_t> next(jobs.size());
+    std::vector<int> k(jobs.size(), 0);
+    for (size_t ji = 0; ji < jobs.size(); ji++) next[ji] = jobs[ji].lo;
+    for (bool more = true; more;) {
+        more = false;
+        for (size_t ji = 0; ji < jobs.size(); ji++) { // round-robin over devices, a chunk each
+            const Job &j = jobs[ji];
+            if (next[ji] >= j.hi) continue;
+            more = true;
+            mk::DevCtx &c = h->dev[j.d];
+            mk::DeviceGuard g(j.d);
+            const int b = k[ji]++ & 1;
+            int rc = drain(ji, b);
+            if (rc) return rc;
+            const size_t lo = next[ji], m = std::min<size_t>(C, j.hi - lo);
+            next[ji] = lo + m;
+            char *hb = (char *)c.h_stage + (size_t)b * c.stage_bytes;
+            char *db = (char *)c.d_stage + (size_t)b * c.stage_bytes;
+            memcpy(hb, in + lo, m * 8);
+            if (hipMemcpyAsync(db, hb, m * 8, hipMemcpyHostToDevice, c.stream) != hipSuccess) return MK_EDEVICE;
+            mk_input mi{};
+            mi.kind = MK_IN_I64;
+            mi.data = db;
+            rc = mk::launch_locked(h, j.d, &mi, m, (int32_t *)(db + a8), (uint8_t *)(db + a8 + a4 + a4),
+                                   steps ? (uint32_t *)(db + a8 + a4) : nullptr, nullptr, opts, c.stream);
+            if (rc) return rc;
+            if (hipMemcpyAsync(hb + a8, db + a8, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+                hipMemcpyAsync(hb + a8 + a4 + a4, db + a8 + a4 + a4, m, hipMemcpyDeviceToHost, c.stream) !=
+                    hipSuccess)
+                return MK_EDEVICE;
+            if (steps && hipMemcpyAsync(hb + a8 + a4, db + a8 + a4, m * 4, hipMemcpyDeviceToHost, c.stream) !=
+                             hipSuccess)
+                return MK_EDEVICE;
+            if (hipEventRecord(c.stage_ev[b], c.stream) != hipSuccess) return MK_EDEVICE;
+            pend[ji][b] = {lo, m, true};
+        }
     }
-    return rc;
+    for (size_t ji = 0; ji < jobs.size(); ji++) {
+        mk::DeviceGuard g(jobs[ji].d);
+        for (int b = 0; b < 2; b++) {
+            int rc = drain(ji, b);
+            if (rc) return rc;
+        }
+    }
+    return MK_OK;
 }
 
 int mk_compute_device(mk_net *h, int device, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,

@@ -601,3 +601,32 @@ def test_lane_trace_matches_oracle(gpu, seed):
         ref, rst = po.trace_lane(onet, x, max_entries=512, **kw)
         assert st == rst, (seed, x, st, rst)
         assert got.tobytes() == ref.tobytes(), (seed, x, got[:8], ref[:8])
+
+
+# The host API streams a batch through pinned staging buffers in chunks
+# (two alternating per device): chunk boundaries, steps on/off, ragged tails.
+@pytest.mark.parametrize("chunk", [1000, 4096])
+def test_host_api_chunks(gpu, monkeypatch, chunk):
+    monkeypatch.setenv("MK_HOST_CHUNK", str(chunk))
+    for nodes, gen in [(mk.networks.countdown_network(), dict(kind=1, mask=1023)),
+                       (mk.networks.pipeline_network(16), {}), (mk.networks.sample_network(), {})]:
+        net = mk.Network(nodes)
+        xs = po.gen_inputs(SEED + chunk, 10007, **gen)
+        ref = oracle(nodes, xs)
+        assert_same(net.compute_batch(xs), ref, f"chunk {chunk}")
+        got = net.compute_batch(xs, steps=False)
+        assert np.array_equal(got.out, ref[0]) and np.array_equal(got.status, ref[1]) and got.steps is None
+
+
+def test_host_api_device_mask(gpu):
+    # device_mask selects the GPUs of an in-process shard; naming a GPU that
+    # does not exist is an error (never a silent fallback)
+    import torch
+
+    net = mk.Network(mk.networks.example_network())
+    xs = po.gen_inputs(SEED, 3000)
+    ndev = torch.cuda.device_count()
+    assert_same(net.compute_batch(xs, devices=range(ndev)), oracle(mk.networks.example_network(), xs), "all GPUs")
+    with pytest.raises(N.MkError) as e:
+        net.compute_batch(xs, devices=[ndev])
+    assert e.value.code == N.MK_EINVAL
