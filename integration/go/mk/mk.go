@@ -26,6 +26,9 @@ const (
 	Program NodeKind = C.MK_NODE_PROGRAM
 	Stack   NodeKind = C.MK_NODE_STACK
 	Master  NodeKind = C.MK_NODE_MASTER
+	// peers of a mixed deployment, served by reference processes (row f4)
+	RemoteProgram NodeKind = C.MK_NODE_REMOTE_PROGRAM
+	RemoteStack   NodeKind = C.MK_NODE_REMOTE_STACK
 )
 
 // Status bits of one /compute result (mk.h MK_ST_*).
@@ -34,6 +37,7 @@ const (
 	Budget        = C.MK_ST_BUDGET
 	StackOverflow = C.MK_ST_STACK_OVERFLOW
 	OutputStop    = C.MK_ST_OUTPUT_STOP
+	RemoteWait    = C.MK_ST_REMOTE_WAIT
 	HasOutput     = C.MK_ST_HAS_OUTPUT
 )
 
@@ -179,4 +183,156 @@ func (s *Sessions) Close() {
 		C.mk_session_free(s.s)
 		s.s = nil
 	}
+}
+
+// ComputeSeq performs len(in)/n sequential /compute calls on every instance
+// in one launch: in[c*n+i] is call c of instance i (mk_session_compute_seq).
+// A master serving concurrent requests on one instance coalesces them here.
+func (s *Sessions) ComputeSeq(in []int) (*Result, error) {
+	if s.n == 0 || len(in)%s.n != 0 {
+		return nil, fmt.Errorf("want a multiple of %d values, got %d", s.n, len(in))
+	}
+	m := len(in)
+	r := &Result{Out: make([]int32, m), Status: make([]uint8, m), Steps: make([]uint32, m)}
+	if m == 0 {
+		return r, nil
+	}
+	in64 := make([]int64, m)
+	for i, v := range in {
+		in64[i] = int64(v)
+	}
+	rc := C.mk_session_compute_seq(s.s, (*C.int64_t)(unsafe.Pointer(&in64[0])), C.size_t(m/s.n),
+		(*C.int32_t)(unsafe.Pointer(&r.Out[0])), (*C.uint8_t)(unsafe.Pointer(&r.Status[0])),
+		(*C.uint32_t)(unsafe.Pointer(&r.Steps[0])))
+	if rc != C.MK_OK {
+		return nil, fmt.Errorf("mk_session_compute_seq: %d", int(rc))
+	}
+	return r, nil
+}
+
+// Step starts a call on instance 0..n-1 (in != nil) or resumes the parked
+// calls of a mixed deployment (in == nil) -- mk_session_step.
+func (s *Sessions) Step(in []int) (*Result, error) {
+	r := &Result{Out: make([]int32, s.n), Status: make([]uint8, s.n), Steps: make([]uint32, s.n)}
+	var p *C.int64_t
+	if in != nil {
+		if len(in) != s.n {
+			return nil, fmt.Errorf("want %d values, got %d", s.n, len(in))
+		}
+		in64 := make([]int64, s.n)
+		for i, v := range in {
+			in64[i] = int64(v)
+		}
+		p = (*C.int64_t)(unsafe.Pointer(&in64[0]))
+	}
+	rc := C.mk_session_step(s.s, p, (*C.int32_t)(unsafe.Pointer(&r.Out[0])),
+		(*C.uint8_t)(unsafe.Pointer(&r.Status[0])), (*C.uint32_t)(unsafe.Pointer(&r.Steps[0])))
+	if rc != C.MK_OK {
+		return nil, fmt.Errorf("mk_session_step: %d", int(rc))
+	}
+	return r, nil
+}
+
+// RemoteRequest is an outstanding Program.Send / Stack.Push / Stack.Pop of a
+// parked call (mk_remote_req).
+type RemoteRequest struct {
+	Node, Op, Remote, Reg uint32
+	Value                 int32
+}
+
+// RemoteRequests lists instance inst's outstanding requests (mk_session_remote_poll).
+func (s *Sessions) RemoteRequests(inst int) ([]RemoteRequest, error) {
+	var reqs [C.MK_MAX_PROGRAM_NODES]C.mk_remote_req
+	var cnt C.int
+	if rc := C.mk_session_remote_poll(s.s, C.size_t(inst), &reqs[0], C.int(len(reqs)), &cnt); rc != C.MK_OK {
+		return nil, fmt.Errorf("mk_session_remote_poll: %d", int(rc))
+	}
+	out := make([]RemoteRequest, int(cnt))
+	for i := range out {
+		r := reqs[i]
+		out[i] = RemoteRequest{uint32(r.node), uint32(r.op), uint32(r.remote), uint32(r.reg), int32(r.value)}
+	}
+	return out, nil
+}
+
+// RemoteDone reports a request's RPC as completed (the popped value for a pop).
+func (s *Sessions) RemoteDone(inst int, node uint32, value int32) error {
+	if rc := C.mk_session_remote_done(s.s, C.size_t(inst), C.uint32_t(node), C.int32_t(value)); rc != C.MK_OK {
+		return fmt.Errorf("mk_session_remote_done: %d", int(rc))
+	}
+	return nil
+}
+
+// PortPut serves a peer's Program.Send into a local port; busy=true while the
+// port is full (program.go:163: the RPC waits).
+func (s *Sessions) PortPut(inst int, node, reg uint32, value int32) (busy bool, err error) {
+	rc := C.mk_session_port_put(s.s, C.size_t(inst), C.uint32_t(node), C.uint32_t(reg), C.int32_t(value))
+	if rc == C.MK_EBUSY {
+		return true, nil
+	}
+	if rc != C.MK_OK {
+		return false, fmt.Errorf("mk_session_port_put: %d", int(rc))
+	}
+	return false, nil
+}
+
+// StackPush / StackPop serve a peer's Stack.Push / Stack.Pop on a local
+// stack; StackPop reports busy while the stack is empty (stack.go:133-155).
+func (s *Sessions) StackPush(inst int, stack uint32, value int32) error {
+	if rc := C.mk_session_stack_push(s.s, C.size_t(inst), C.uint32_t(stack), C.int32_t(value)); rc != C.MK_OK {
+		return fmt.Errorf("mk_session_stack_push: %d", int(rc))
+	}
+	return nil
+}
+
+func (s *Sessions) StackPop(inst int, stack uint32) (value int32, busy bool, err error) {
+	var v C.int32_t
+	rc := C.mk_session_stack_pop(s.s, C.size_t(inst), C.uint32_t(stack), &v)
+	if rc == C.MK_EBUSY {
+		return 0, true, nil
+	}
+	if rc != C.MK_OK {
+		return 0, false, fmt.Errorf("mk_session_stack_pop: %d", int(rc))
+	}
+	return int32(v), false, nil
+}
+
+// NodeIndex is mk_net_node_index: the kind and index of a node by name.
+func (n *Net) NodeIndex(name string) (NodeKind, int, error) {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var kind, idx C.int
+	if rc := C.mk_net_node_index(n.h, cs, &kind, &idx); rc != C.MK_OK {
+		return 0, 0, fmt.Errorf("mk_net_node_index %q: %d", name, int(rc))
+	}
+	return NodeKind(kind), int(idx), nil
+}
+
+// TraceEntry is one retired instruction of a traced lane (mk_trace_entry).
+type TraceEntry struct {
+	Round    uint32
+	Node, IP uint16
+	Acc, Bak int64
+}
+
+// Trace runs one /compute input through the interpreter and returns its
+// first max retired instructions (mk_trace_lane) -- the reference's
+// per-instruction log.Printf (program.go:222-223) as data.
+func (n *Net) Trace(device int, input int, max int, opts Options) ([]TraceEntry, uint8, error) {
+	if max <= 0 {
+		return nil, 0, fmt.Errorf("max must be positive")
+	}
+	buf := make([]C.mk_trace_entry, max)
+	o := opts.c()
+	var cnt C.uint32_t
+	var st C.uint8_t
+	if rc := C.mk_trace_lane(n.h, C.int(device), C.int64_t(input), &o, &buf[0], C.uint32_t(max), &cnt, &st); rc != C.MK_OK {
+		return nil, 0, fmt.Errorf("mk_trace_lane: %d", int(rc))
+	}
+	out := make([]TraceEntry, int(cnt))
+	for i := range out {
+		e := buf[i]
+		out[i] = TraceEntry{uint32(e.round), uint16(e.node), uint16(e.ip), int64(e.acc), int64(e.bak)}
+	}
+	return out, uint8(st), nil
 }

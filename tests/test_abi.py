@@ -56,6 +56,6 @@ def test_go_adapter_binds_only_declared_symbols():
     # the C ABI through cgo; every C.mk_* it names must exist in include/mk.h
     src = open(os.path.join(ROOT, "integration", "go", "mk", "mk.go")).read()
     used = set(re.findall(r"\bC\.(mk_[a-z_0-9]+)\b", src))
-    types = {"mk_net", "mk_session", "mk_opts", "mk_node_desc"}
+    types = {"mk_net", "mk_session", "mk_opts", "mk_node_desc", "mk_remote_req", "mk_trace_entry"}
     assert used - types <= set(declared_functions()), used - types - set(declared_functions())
     assert {"mk_net_load", "mk_compute_batch", "mk_session_create", "mk_session_compute"} <= used
