@@ -1106,6 +1106,89 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     p.out_val[gid] = out_val;
 }
 
+// ---- input order for the machine shape (tier 3) -----------------------------
+// A wave of the machine-shape kernel runs 64 lanes together and each
+// data-dependent loop until the wave's longest trip: lanes with similar
+// inputs, whose trips are similar, waste less.  Before such a launch the
+// input indices are grouped by value -- a counting sort into kOrderBuckets
+// buckets over [min, max] of the batch -- and lane j answers input order[j].
+// Every input is still evaluated exactly once and answered at its own index:
+// only which lanes share a wave changes.
+constexpr uint32_t kOrderBuckets = 4096;
+constexpr uint64_t kOrderMin = 65536; // smaller batches launch unordered
+
+__device__ __forceinline__ uint32_t order_bucket(int32_t v, int32_t lo, int32_t hi)
+{
+    const uint64_t span = (uint64_t)((int64_t)hi - (int64_t)lo) + 1u;
+    return (uint32_t)(((uint64_t)((int64_t)v - (int64_t)lo) * kOrderBuckets) / span);
+}
+
+// tab: [0] min, [1] max, [2 ..] buckets
+__global__ void __launch_bounds__(256) order_minmax(SParams p, int32_t *tab)
+{
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * 256u) {
+        const int32_t v = sched_input(p, i);
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        atomicMin(&tab[0], lo);
+        atomicMax(&tab[1], hi);
+    }
+}
+
+__global__ void __launch_bounds__(256) order_hist(SParams p, int32_t *tab)
+{
+    __shared__ uint32_t h[kOrderBuckets];
+    for (uint32_t b = threadIdx.x; b < kOrderBuckets; b += 256u) h[b] = 0u;
+    __syncthreads();
+    const int32_t lo = tab[0], hi = tab[1];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * 256u)
+        atomicAdd(&h[order_bucket(sched_input(p, i), lo, hi)], 1u);
+    __syncthreads();
+    uint32_t *g = (uint32_t *)(tab + 2);
+    for (uint32_t b = threadIdx.x; b < kOrderBuckets; b += 256u)
+        if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+// exclusive prefix sum of the buckets, in place (one block of 1024)
+__global__ void __launch_bounds__(1024) order_scan(int32_t *tab)
+{
+    __shared__ uint32_t part[1024];
+    uint32_t *g = (uint32_t *)(tab + 2);
+    const uint32_t t = threadIdx.x, per = kOrderBuckets / 1024u;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k) sum += g[t * per + k];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024u; o <<= 1) {
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t c = g[t * per + k];
+        g[t * per + k] = run;
+        run += c;
+    }
+}
+
+__global__ void __launch_bounds__(256) order_scatter(SParams p, int32_t *tab, uint32_t *order)
+{
+    const int32_t lo = tab[0], hi = tab[1];
+    uint32_t *g = (uint32_t *)(tab + 2);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * 256u)
+        order[atomicAdd(&g[order_bucket(sched_input(p, i), lo, hi)], 1u)] = (uint32_t)i;
+}
+
 __global__ void __launch_bounds__(kBlock) gen_inputs(uint64_t seed, uint32_t kind, uint32_t mask,
                                                      uint64_t offset, uint64_t n, int32_t *out)
 {
@@ -1148,6 +1231,9 @@ struct SchedDev {
     uint32_t *d_jtab = nullptr;
     int32_t *d_slots = nullptr;
     size_t slots_bytes = 0;
+    uint32_t *d_order = nullptr; // machine shape: input order of a launch (order_* kernels)
+    size_t order_cap = 0;
+    int32_t *d_ordtab = nullptr; // min, max, buckets
 };
 
 // Tier 3: the schedule compiled to a native kernel (tis_jit.h).
@@ -1239,6 +1325,8 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_entry);
                 (void)hipFree(sc->dev[d].d_jtab);
                 (void)hipFree(sc->dev[d].d_slots);
+                (void)hipFree(sc->dev[d].d_order);
+                (void)hipFree(sc->dev[d].d_ordtab);
                 if (sc->jit.dev[d].mod) (void)hipModuleUnload(sc->jit.dev[d].mod);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
@@ -1717,6 +1805,31 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     const uintptr_t va = 4u * kJitStreamLanes;
     p.io_vec = in->kind == MK_IN_I32 && (uintptr_t)in->data % va == 0 && (uintptr_t)d_out % va == 0 &&
                (uintptr_t)d_status % kJitStreamLanes == 0 && (uintptr_t)d_steps % va == 0;
+    p.order = nullptr;
+    if (sc->jit.shape == JIT_MACHINE && !sc->jit.pool && h->jit_lim.order && n >= kOrderMin && n < (1ull << 32)) {
+        // group the inputs by value (order_* kernels): lanes of a wave get similar trips
+        if (n > sd.order_cap) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(sd.d_order);
+            sd.d_order = nullptr;
+            sd.order_cap = 0;
+            if (hipMalloc(&sd.d_order, n * sizeof(uint32_t)) != hipSuccess) return MK_ENOMEM;
+            sd.order_cap = n;
+        }
+        if (!sd.d_ordtab && hipMalloc(&sd.d_ordtab, (2 + kOrderBuckets) * sizeof(int32_t)) != hipSuccess)
+            return MK_ENOMEM;
+        const int32_t init[2] = {INT32_MAX, INT32_MIN};
+        const int grid = std::max(1, std::min(c.cus * 8, (int)((n + 255) / 256)));
+        if (hipMemsetAsync(sd.d_ordtab + 2, 0, kOrderBuckets * sizeof(int32_t), stream) != hipSuccess ||
+            hipMemcpyAsync(sd.d_ordtab, init, sizeof init, hipMemcpyHostToDevice, stream) != hipSuccess)
+            return MK_EDEVICE;
+        hipLaunchKernelGGL(order_minmax, dim3(grid), dim3(256), 0, stream, p, sd.d_ordtab);
+        hipLaunchKernelGGL(order_hist, dim3(grid), dim3(256), 0, stream, p, sd.d_ordtab);
+        hipLaunchKernelGGL(order_scan, dim3(1), dim3(1024), 0, stream, sd.d_ordtab);
+        hipLaunchKernelGGL(order_scatter, dim3(grid), dim3(256), 0, stream, p, sd.d_ordtab, sd.d_order);
+        if (hipGetLastError() != hipSuccess) return MK_EDEVICE;
+        p.order = sd.d_order;
+    }
     uint64_t s0 = 0;
     do {
         SParams q = p;

@@ -1451,25 +1451,29 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
     const uint32_t refill_t = pol & 0xffu;
     unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    // lane j answers input ord(j): the identity, or (p.order) the inputs
+    // grouped by value, so that a wave's lanes have similar loop trip counts
+#define MK_ORD(j) (p.order ? (uint64_t)p.order[j] : (j))
     uint64_t idx = gid;
     MkLane L;
-    mk_init(L, idx < p.n ? sched_input(p, idx) : 0);
+    mk_init(L, idx < p.n ? sched_input(p, MK_ORD(idx)) : 0);
     if (idx >= p.n) L.sb = MK_SB_IDLE;
-    int32_t nxt = idx + stride < p.n ? sched_input(p, idx + stride) : 0;
+    int32_t nxt = idx + stride < p.n ? sched_input(p, MK_ORD(idx + stride)) : 0;
     for (;;) {
         const bool fin = L.sb == MK_SB_DONE;
         const unsigned long long finb = __ballot(fin);
         unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
         if (finb && (!actb || (uint32_t)__popcll(finb) >= refill_t)) {
             if (fin) {
-                p.out[idx] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
-                p.status[idx] = (uint8_t)L.st;
-                if (p.steps) p.steps[idx] = L.steps;
+                const uint64_t at = MK_ORD(idx);
+                p.out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+                p.status[at] = (uint8_t)L.st;
+                if (p.steps) p.steps[at] = L.steps;
                 count_lane(cnt, L.steps, L.st);
                 idx += stride;
                 if (idx < p.n) {
                     mk_init(L, nxt);
-                    nxt = idx + stride < p.n ? sched_input(p, idx + stride) : 0;
+                    nxt = idx + stride < p.n ? sched_input(p, MK_ORD(idx + stride)) : 0;
                 } else {
                     L.sb = MK_SB_IDLE;
                 }
@@ -1524,6 +1528,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_SLOT_NT", l.slot_nt);
     flag("MK_JIT_IO_NT", l.io_nt);
     num("MK_JIT_POOL", l.pool);
+    flag("MK_JIT_ORDER", l.order);
     return l;
 }
 
@@ -1531,9 +1536,9 @@ std::string JitLimits::key() const
 {
     char b[256];
     snprintf(b, sizeof b,
-             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u",
+             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
-             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool);
+             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order);
     return b;
 }
 

@@ -77,6 +77,10 @@ struct JitLimits {
     //         dispatch (kMachinePoolKernel).
     // Both compaction kernels are bit-exact and slower on C5.
     uint32_t pool = 0;
+    // Machine shape: run the inputs grouped by value (a counting sort of the
+    // batch's indices before the launch), so that a wave's lanes have
+    // similar loop trip counts (MK_JIT_ORDER=0: input order).
+    bool order = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key

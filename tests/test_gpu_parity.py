@@ -630,3 +630,39 @@ def test_host_api_device_mask(gpu):
     with pytest.raises(N.MkError) as e:
         net.compute_batch(xs, devices=[ndev])
     assert e.value.code == N.MK_EINVAL
+
+
+# Machine-shape launches of >= 64K inputs run the inputs grouped by value
+# (order_* kernels, lane j answers input order[j]); every input is answered
+# at its own index, identically to the input-order launch (MK_JIT_ORDER=0).
+@pytest.mark.parametrize("kind", ["gen", "i32", "i64"])
+def test_machine_input_order_is_transparent(gpu, monkeypatch, kind):
+    import torch
+
+    n = 200_003
+    cases = [("c5", mk.networks.countdown_network(), (N.MK_GEN_MASKED, 1023))]
+    for seed in (3, 17, 41):
+        rows = random_network(seed)
+        cases.append((f"seed{seed}", rows, (N.MK_GEN_FULL, 0)))
+    for label, nodes, gen in cases:
+        res = {}
+        for order in ("1", "0"):
+            monkeypatch.setenv("MK_JIT_ORDER", order)
+            net = mk.Network(nodes)
+            if "shape=machine" not in net.plan():
+                monkeypatch.setenv("MK_JIT_SHAPE", "machine")
+                net = mk.Network(nodes)
+                monkeypatch.delenv("MK_JIT_SHAPE")
+            xs = torch.from_numpy(po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1]))
+            if kind == "gen":
+                res[order] = _device_run(net, n, gen=gen)
+            elif kind == "i32":
+                res[order] = _device_run(net, n, in_tensor=xs.to(torch.int32).cuda(), in_kind=N.MK_IN_I32)
+            else:
+                res[order] = _device_run(net, n, in_tensor=xs.cuda(), in_kind=N.MK_IN_I64)
+        for a, b in zip(res["1"], res["0"]):
+            assert np.array_equal(a, b), label
+        ref = oracle(nodes, po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1])[-3000:])
+        out, st, sp, _ = res["1"]
+        assert np.array_equal(out[-3000:], ref[0]) and np.array_equal(st[-3000:], ref[1]) and \
+            np.array_equal(sp[-3000:], ref[2]), label
