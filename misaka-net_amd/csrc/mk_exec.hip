@@ -1275,13 +1275,11 @@ struct DevCtx {
     int cus = 0;
     int32_t *d_spill = nullptr;
     size_t spill_bytes = 0;
-    // host-API staging (mk_compute_batch): two chunk buffers on the device
-    // and their pinned host mirrors, so a chunk's host copies overlap the
-    // previous chunk's transfers and launch
+    // host-API staging (mk_compute_batch): device buffers for one call's
+    // share, and a pinned host mirror while that share fits one chunk
     void *d_stage = nullptr;
     void *h_stage = nullptr;
-    size_t stage_bytes = 0;        // per buffer
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
     unsigned long long *d_partials = nullptr; // per-wave counters
     size_t partials_bytes = 0;
     hipStream_t stream = nullptr;
@@ -1317,8 +1315,6 @@ struct mk_net {
             (void)hipFree(c.d_spill);
             (void)hipFree(c.d_stage);
             (void)hipHostFree(c.h_stage);
-            for (hipEvent_t e : c.stage_ev)
-                if (e) (void)hipEventDestroy(e);
             (void)hipFree(c.d_partials);
             for (auto &sc : sched) {
                 (void)hipFree(sc->dev[d].d_code);
@@ -1725,8 +1721,8 @@ int ensure_jit_device(SchedCache *sc, int d)
     return MK_OK;
 }
 
-// Host-API chunk (inputs per pinned staging buffer, 4M); MK_HOST_CHUNK
-// overrides it for networks loaded afterwards (tests: many chunks per batch).
+// Host-API calls of up to this many inputs per device stage through pinned
+// memory (4M); MK_HOST_CHUNK overrides it for networks loaded afterwards.
 uint64_t host_chunk_from_env()
 {
     const char *e = std::getenv("MK_HOST_CHUNK");
@@ -2089,99 +2085,83 @@ int mk_compute_batch(mk_net *h, const int64_t *in, size_t n, int32_t *out, uint8
             devs.push_back(d);
         }
     const size_t G = devs.size();
-    // Each device's range goes through in chunks: host values are copied
-    // into pinned buffers (two per device, alternating), moved by DMA, run,
-    // and the results copied back out of pinned memory -- the host copies of
-    // one chunk overlap the transfers and launch of the other.
     struct Job { int d; size_t lo, hi; };
     std::vector<Job> jobs;
     for (size_t g = 0; g < G; g++) {
         const size_t lo = n * g / G, hi = n * (g + 1) / G;
         if (hi > lo) jobs.push_back({devs[g], lo, hi});
     }
+    // Transfers: a device's share up to one chunk (h->host_chunk inputs, the
+    // master's bursts and other latency-bound calls) goes through pinned
+    // staging, so each copy is one DMA with no runtime staging or extra sync;
+    // larger shares go straight from the caller's pageable buffers, where the
+    // runtime's own pipelined staging moves more bytes per second than one
+    // host thread copying into pinned memory (C2, 16M lanes: 9.7 ms per call
+    // pageable vs 13.2 ms through a single-threaded pinned double buffer).
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t C = (size_t)std::min<uint64_t>(h->host_chunk, n);
-    const size_t a8 = al(C * 8), a4 = al(C * 4), a1 = al(C);
-    const size_t per = a8 + a4 + a4 + a1; // in, out, steps, status
     for (auto &j : jobs) {
         int rc = mk::ensure_device(h, j.d);
         if (rc) return rc;
         mk::DevCtx &c = h->dev[j.d];
         mk::DeviceGuard g(j.d);
-        if (per > c.stage_bytes) {
+        const size_t m = j.hi - j.lo;
+        const bool pinned = m <= h->host_chunk;
+        const size_t a8 = al(m * 8), a4 = al(m * 4), a1 = al(m);
+        const size_t need = a8 + a4 + a4 + a1; // in, out, steps, status
+        if (need > c.stage_bytes || (pinned && !c.h_stage)) {
             (void)hipStreamSynchronize(c.stream);
             (void)hipFree(c.d_stage);
             (void)hipHostFree(c.h_stage);
             c.d_stage = c.h_stage = nullptr;
             c.stage_bytes = 0;
-            if (hipMalloc(&c.d_stage, 2 * per) != hipSuccess) return MK_ENOMEM;
-            if (hipHostMalloc(&c.h_stage, 2 * per, hipHostMallocDefault) != hipSuccess) return MK_ENOMEM;
-            c.stage_bytes = per;
+            const size_t sz = std::max(need, c.stage_bytes);
+            if (hipMalloc(&c.d_stage, sz) != hipSuccess) return MK_ENOMEM;
+            if (sz <= al(h->host_chunk * 8) + 2 * al(h->host_chunk * 4) + al(h->host_chunk) &&
+                hipHostMalloc(&c.h_stage, sz, hipHostMallocDefault) != hipSuccess)
+                return MK_ENOMEM;
+            c.stage_bytes = sz;
         }
-        for (hipEvent_t &e : c.stage_ev)
-            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
-    }
-    // per device: chunk k uses buffer k & 1; before a buffer is refilled its
-    // previous chunk's results are copied out (after its event)
-    struct Pend { size_t lo = 0, m = 0; bool live = false; };
-    std::vector<std::array<Pend, 2>> pend(jobs.size());
-    auto drain = [&](size_t ji, int b) -> int {
-        Pend &q = pend[ji][b];
-        if (!q.live) return MK_OK;
-        mk::DevCtx &c = h->dev[jobs[ji].d];
-        if (hipEventSynchronize(c.stage_ev[b]) != hipSuccess) return MK_EDEVICE;
-        const char *hb = (const char *)c.h_stage + (size_t)b * c.stage_bytes;
-        memcpy(out + q.lo, hb + a8, q.m * 4);
-        if (steps) memcpy(steps + q.lo, hb + a8 + a4, q.m * 4);
-        memcpy(status + q.lo, hb + a8 + a4 + a4, q.m);
-        q.live = false;
-        return MK_OK;
-    };
-    std::vector<size_t> next(jobs.size());
-    std::vector<int> k(jobs.size(), 0);
-    for (size_t ji = 0; ji < jobs.size(); ji++) next[ji] = jobs[ji].lo;
-    for (bool more = true; more;) {
-        more = false;
-        for (size_t ji = 0; ji < jobs.size(); ji++) { // round-robin over devices, a chunk each
-            const Job &j = jobs[ji];
-            if (next[ji] >= j.hi) continue;
-            more = true;
-            mk::DevCtx &c = h->dev[j.d];
-            mk::DeviceGuard g(j.d);
-            const int b = k[ji]++ & 1;
-            int rc = drain(ji, b);
-            if (rc) return rc;
-            const size_t lo = next[ji], m = std::min<size_t>(C, j.hi - lo);
-            next[ji] = lo + m;
-            char *hb = (char *)c.h_stage + (size_t)b * c.stage_bytes;
-            char *db = (char *)c.d_stage + (size_t)b * c.stage_bytes;
-            memcpy(hb, in + lo, m * 8);
+        char *db = (char *)c.d_stage;
+        char *hb = pinned && c.h_stage ? (char *)c.h_stage : nullptr;
+        if (hb) {
+            memcpy(hb, in + j.lo, m * 8);
             if (hipMemcpyAsync(db, hb, m * 8, hipMemcpyHostToDevice, c.stream) != hipSuccess) return MK_EDEVICE;
-            mk_input mi{};
-            mi.kind = MK_IN_I64;
-            mi.data = db;
-            rc = mk::launch_locked(h, j.d, &mi, m, (int32_t *)(db + a8), (uint8_t *)(db + a8 + a4 + a4),
-                                   steps ? (uint32_t *)(db + a8 + a4) : nullptr, nullptr, opts, c.stream);
-            if (rc) return rc;
-            if (hipMemcpyAsync(hb + a8, db + a8, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
-                hipMemcpyAsync(hb + a8 + a4 + a4, db + a8 + a4 + a4, m, hipMemcpyDeviceToHost, c.stream) !=
-                    hipSuccess)
-                return MK_EDEVICE;
-            if (steps && hipMemcpyAsync(hb + a8 + a4, db + a8 + a4, m * 4, hipMemcpyDeviceToHost, c.stream) !=
-                             hipSuccess)
-                return MK_EDEVICE;
-            if (hipEventRecord(c.stage_ev[b], c.stream) != hipSuccess) return MK_EDEVICE;
-            pend[ji][b] = {lo, m, true};
+        } else if (hipMemcpyAsync(db, in + j.lo, m * 8, hipMemcpyHostToDevice, c.stream) != hipSuccess) {
+            return MK_EDEVICE;
+        }
+        mk_input mi{};
+        mi.kind = MK_IN_I64;
+        mi.data = db;
+        rc = mk::launch_locked(h, j.d, &mi, m, (int32_t *)(db + a8), (uint8_t *)(db + a8 + a4 + a4),
+                               steps ? (uint32_t *)(db + a8 + a4) : nullptr, nullptr, opts, c.stream);
+        if (rc) return rc;
+        char *o = hb ? hb + a8 : (char *)(out + j.lo);
+        char *st = hb ? hb + a8 + a4 + a4 : (char *)(status + j.lo);
+        char *sp = hb ? hb + a8 + a4 : (char *)(steps ? steps + j.lo : nullptr);
+        if (hipMemcpyAsync(o, db + a8, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+            hipMemcpyAsync(st, db + a8 + a4 + a4, m, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
+            return MK_EDEVICE;
+        if (steps && hipMemcpyAsync(sp, db + a8 + a4, m * 4, hipMemcpyDeviceToHost, c.stream) != hipSuccess)
+            return MK_EDEVICE;
+    }
+    int rc = MK_OK;
+    for (auto &j : jobs) { // drain every device, then copy pinned results out
+        mk::DevCtx &c = h->dev[j.d];
+        mk::DeviceGuard g(j.d);
+        if (hipStreamSynchronize(c.stream) != hipSuccess) {
+            rc = MK_EDEVICE;
+            continue;
+        }
+        const size_t m = j.hi - j.lo;
+        if (m <= h->host_chunk && c.h_stage) {
+            const char *hb = (const char *)c.h_stage;
+            const size_t a8 = al(m * 8), a4 = al(m * 4);
+            memcpy(out + j.lo, hb + a8, m * 4);
+            if (steps) memcpy(steps + j.lo, hb + a8 + a4, m * 4);
+            memcpy(status + j.lo, hb + a8 + a4 + a4, m);
         }
     }
-    for (size_t ji = 0; ji < jobs.size(); ji++) {
-        mk::DeviceGuard g(jobs[ji].d);
-        for (int b = 0; b < 2; b++) {
-            int rc = drain(ji, b);
-            if (rc) return rc;
-        }
-    }
-    return MK_OK;
+    return rc;
 }
 
 int mk_compute_device(mk_net *h, int device, const mk_input *in, size_t n, int32_t *d_out, uint8_t *d_status,

@@ -603,15 +603,18 @@ def test_lane_trace_matches_oracle(gpu, seed):
         assert got.tobytes() == ref.tobytes(), (seed, x, got[:8], ref[:8])
 
 
-# The host API streams a batch through pinned staging buffers in chunks
-# (two alternating per device): chunk boundaries, steps on/off, ragged tails.
+# The host API stages calls of up to MK_HOST_CHUNK inputs through pinned
+# memory and larger ones straight from the caller's buffers: both paths,
+# alternating on one handle (buffers are re-sized), steps on and off.
 @pytest.mark.parametrize("chunk", [1000, 4096])
 def test_host_api_chunks(gpu, monkeypatch, chunk):
     monkeypatch.setenv("MK_HOST_CHUNK", str(chunk))
-    for nodes, gen in [(mk.networks.countdown_network(), dict(kind=1, mask=1023)),
-                       (mk.networks.pipeline_network(16), {}), (mk.networks.sample_network(), {})]:
+    for (nodes, gen), n in zip([(mk.networks.countdown_network(), dict(kind=1, mask=1023)),
+                                (mk.networks.pipeline_network(16), {}), (mk.networks.sample_network(), {}),
+                                (mk.networks.countdown_network(), dict(kind=1, mask=1023))],
+                               [10007, chunk, 977, 10007]):
         net = mk.Network(nodes)
-        xs = po.gen_inputs(SEED + chunk, 10007, **gen)
+        xs = po.gen_inputs(SEED + chunk + n, n, **gen)
         ref = oracle(nodes, xs)
         assert_same(net.compute_batch(xs), ref, f"chunk {chunk}")
         got = net.compute_batch(xs, steps=False)
