@@ -1848,6 +1848,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
 }
 
 enum Tier { TIER_NONE, TIER_INTERP, TIER_COMPILED, TIER_NATIVE };
+constexpr uint32_t kSchedInterpSb = 1024; // above: tier 1 instead of tier 2 (pick_tier)
 
 // Caller holds h->mu.  The tier a launch with `flags` runs on: tier 1 when
 // forced; else the native kernel unless tier 2 was asked for (TILE/REFILL);
@@ -1864,6 +1865,12 @@ Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, uint32_t budget, SchedCa
     if (want_jit && jit_compile(sc, h->jit_lim) && (sc->jit.shape == JIT_MACHINE || (uint64_t)budget > sc->jit.max_steps))
         return TIER_NATIVE;
     if (flags & MK_FLAG_JIT) return TIER_NONE;
+    // A schedule with thousands of superblocks is control state that follows
+    // the data (a stack depth per state): tier 2 would dispatch nearly one
+    // superblock per lane, and the interpreter is faster (census class
+    // data_dependent_stack_depth, 4,098 superblocks: 0.016 T node-instr/s on
+    // tier 2, 0.080 T on tier 1).  TILE / REFILL still demand tier 2.
+    if (sc->ok && sc->prog.nsb > kSchedInterpSb && !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL))) return TIER_INTERP;
     return sc->ok ? TIER_COMPILED : TIER_INTERP;
 }
 
@@ -2598,7 +2605,11 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     mk::SchedCache *sc = nullptr;
     const mk::Tier t = mk::pick_tier(h, cap, flags, budget, &sc);
     if (t == mk::TIER_INTERP) {
-        snprintf(buf, sizeof buf, "tier=interp reason=%s", sc ? sc->why.c_str() : "forced");
+        if (sc && sc->ok)
+            snprintf(buf, sizeof buf, "tier=interp reason=compiled schedule of %u superblocks (control state follows "
+                     "the data); native tier: %s", sc->prog.nsb, sc->jit.why.c_str());
+        else
+            snprintf(buf, sizeof buf, "tier=interp reason=%s", sc ? sc->why.c_str() : "forced");
         return mk::copy_out(out, out_len, buf);
     }
     if (t == mk::TIER_NONE) {

@@ -192,7 +192,7 @@ int mkc_tier(void *hv, uint32_t cap, int soo, char *why, size_t why_len)
             tier = 3;
             w = sh == mk::JIT_MACHINE ? (pool ? "machine-pool" : "machine") : heavy ? "stream-heavy" : "stream";
         } else {
-            tier = 2;
+            tier = P.nsb > 1024 ? 1 : 2; // mk_exec.hip pick_tier: kSchedInterpSb
         }
     }
     if (why && why_len) {
