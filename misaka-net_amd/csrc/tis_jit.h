@@ -79,8 +79,10 @@ struct JitLimits {
     uint32_t pool = 0;
     // Machine shape: run the inputs grouped by value (a counting sort of the
     // batch's indices before the launch), so that a wave's lanes have
-    // similar loop trip counts (MK_JIT_ORDER=0: input order).
-    bool order = true;
+    // similar loop trip counts (MK_JIT_ORDER=1).  Off by default: on C5 the
+    // sort's contended bucket atomics and the scattered result writes cost
+    // more than the idle lanes it saves (780 vs 367 us, r02g).
+    bool order = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
