@@ -47,8 +47,8 @@ WORKLOADS = {
     "c4d256": ("c4_pipeline_d256_512K", lambda: mk.networks.pipeline_network(256), 1 << 19, N.MK_GEN_FULL, 0),
     "c4d1024": ("c4_pipeline_d1024_256K", lambda: mk.networks.pipeline_network(1024), 1 << 18, N.MK_GEN_FULL, 0),
     "c5": ("c5_countdown_4M", mk.networks.countdown_network, 1 << 22, N.MK_GEN_MASKED, 1023),
-    # tier census classes (networks.census_classes) that the native tier does not take:
-    # data-dependent stack depth (tier 2) and two independent stack depths (tier 1)
+    # tier census classes (networks.census_classes) whose stack depths follow the
+    # data: until r02i tier 2 / tier 1, now dynamic stacks on the native tier
     "t2_dyn_depth": ("t2_dyn_depth_1M", lambda: mk.networks.census_classes()["data_dependent_stack_depth"][0][1],
                      1 << 20, N.MK_GEN_MASKED, 255),
     "t1_two_stacks": ("t1_two_stacks_1M",
@@ -58,7 +58,11 @@ WORKLOADS = {
 # Stack-node traffic per lane (PUSH + POP, 4 bytes each), part of the
 # algorithmic bytes: the pipeline's 8 nodes each push `depth` values and pop
 # them all (networks.pipeline_program); the other networks have no stacks.
-STACK_OPS_PER_LANE = {"c4": 2 * 64 * 8, "c4d256": 2 * 256 * 8, "c4d1024": 2 * 1024 * 8}
+# The census classes push x values (dyn_depth: and pop them; two_stacks: x
+# onto each of two stacks) for inputs x uniform in 0..255: 2 * 127.5 slot
+# accesses per lane in expectation.
+STACK_OPS_PER_LANE = {"c4": 2 * 64 * 8, "c4d256": 2 * 256 * 8, "c4d1024": 2 * 1024 * 8,
+                      "t2_dyn_depth": 255, "t1_two_stacks": 255}
 
 
 def log(*a):

@@ -423,7 +423,7 @@ __device__ __forceinline__ DOp run_data(const DOp *__restrict__ code, uint32_t &
 {
     for (;;) {
         const DOp I = fetch_dop(code, pc);
-        if (I.op > U_LD) return I;
+        if (I.op > U_DATA_LAST) return I;
         if (I.op <= U_RSUBI) { // MOV LI ADD SUB ADDI RSUBI: int64 arithmetic on registers
             int64_t v[K];
             if (I.op == U_LI) {
@@ -469,6 +469,32 @@ __device__ __forceinline__ DOp run_data(const DOp *__restrict__ code, uint32_t &
             } else {
 #pragma unroll
                 for (int k = 0; k < K; ++k) S.at(mine[k] ? I.d : p.scratch_off)[k * B] = v[k];
+            }
+        } else if (I.op == U_LDX) { // dynamic stack: slot imm + R[b]
+            int64_t x[K], v[K];
+            load_slots<K, B>(S, I.b, 0, x);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                // slots outside the group may hold any index: they read the scratch row
+                const uint64_t row = (FULL || mine[k]) ? (uint64_t)I.imm + (uint64_t)x[k] : p.scratch_slot;
+                v[k] = p.slots[row * p.vlanes + vlane0 + (uint64_t)k * p.lanes];
+            }
+            if (FULL) {
+                int64_t *d = S.at(I.d);
+#pragma unroll
+                for (int k = 0; k < K; ++k) d[k * B] = v[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) S.at(mine[k] ? I.d : p.scratch_off)[k * B] = v[k];
+            }
+        } else if (I.op == U_STX) {
+            int64_t x[K], v[K];
+            load_slots<K, B>(S, I.b, 0, x);
+            load_slots<K, B>(S, I.a, I.fl & UF_TA, v);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint64_t row = (FULL || mine[k]) ? (uint64_t)I.imm + (uint64_t)x[k] : p.scratch_slot;
+                p.slots[row * p.vlanes + vlane0 + (uint64_t)k * p.lanes] = (int32_t)v[k];
             }
         } else { // ST / STI: stack entry to its HBM slot
             int64_t v[K];
@@ -544,8 +570,34 @@ __device__ __forceinline__ void apply_exit(const DOp &E, const uint32_t *__restr
     }
 }
 
+// OVF (a PUSH onto a dynamic stack): the slots of the group whose depth
+// register is at the limit end with the op's status.  Returns whether any
+// slot of the wave is still in the group; `cut` = some slot left it.
+template <int K, int B>
+__device__ __forceinline__ bool apply_ovf(const DOp &E, const Slots<K, B> &S, bool (&mine)[K], uint32_t (&steps)[K],
+                                          bool (&done)[K], uint32_t (&st)[K], int32_t (&outv)[K], bool &cut)
+{
+    const int64_t *a = S.at(E.a), *x = S.at(E.b);
+    const uint64_t lim = (uint64_t)E.imm >> 32;
+    bool left = false, stop_any = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool stop = mine[k] && (uint64_t)x[k * B] >= lim;
+        const int32_t o = (E.fl & UF_OUTREG) ? (int32_t)sx32(a[k * B], E.fl & UF_TA) : (int32_t)(uint32_t)E.imm;
+        steps[k] += stop ? E.inc : 0u;
+        outv[k] = stop ? o : outv[k];
+        st[k] = stop ? E.d : st[k];
+        done[k] = done[k] || stop;
+        mine[k] = mine[k] && !stop;
+        left = left || mine[k];
+        stop_any = stop_any || stop;
+    }
+    cut = __ballot(stop_any) != 0;
+    return __ballot(left) != 0;
+}
+
 // Budget-checked variant (taken only by groups that could reach the budget
-// inside a superblock): ROUND_END may stop single slots.
+// inside a superblock): ROUND_END and OVF may stop single slots.
 template <int K, int B>
 __device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__restrict__ jtab, uint32_t pc,
                             const SParams &p, const Slots<K, B> &S, uint64_t vlane0, bool (&mine)[K],
@@ -569,6 +621,12 @@ __device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__rest
                 left = left || mine[k];
             }
             if (!__ballot(left)) return;
+            ++pc;
+            continue;
+        }
+        if (E.op == U_OVF) {
+            bool cut;
+            if (!apply_ovf<K, B>(E, S, mine, steps, done, st, outv, cut)) return;
             ++pc;
             continue;
         }
@@ -607,7 +665,7 @@ __device__ __forceinline__ bool sched_step(const DOp *__restrict__ code, const u
         mine_any = mine_any || mine[k];
         mine_all = mine_all && mine[k];
     }
-    const bool full = __ballot(mine_any && !mine_all) == 0;
+    bool full = __ballot(mine_any && !mine_all) == 0;
     if (!mine_any) return true;
     uint32_t pc = rfl(entry[u]);
     if (u & 1u) {
@@ -628,6 +686,13 @@ __device__ __forceinline__ bool sched_step(const DOp *__restrict__ code, const u
                 for (int k = 0; k < K; ++k) sb[k] = mine[k] ? (uint32_t)E.imm : sb[k];
                 return true;
             }
+            ++pc;
+            continue;
+        }
+        if (E.op == U_OVF) {
+            bool cut;
+            if (!apply_ovf<K, B>(E, S, mine, steps, fin, st, outv, cut)) return true;
+            full = full && !cut;
             ++pc;
             continue;
         }

@@ -4,6 +4,8 @@
 // the CPU oracle without a GPU.  It is not part of the product library and
 // no product entry point can reach it.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -70,8 +72,15 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
         int32_t outv = 0;
         bool done = false;
         uint64_t guard_words = 0;
+        const char *tr = getenv("MKC_TRACE"); // debugging: trace lane i's superblocks
+        const bool trace = tr && (size_t)atoll(tr) == i;
         while (!done) {
             uint32_t pc = entry[sb];
+            if (trace) {
+                fprintf(stderr, "sb%u%s steps=%u R:", sb / 2, (sb & 1) ? "c" : "", steps);
+                for (size_t r = 0; r < R.size(); r++) fprintf(stderr, " %lld", (long long)R[r]);
+                fprintf(stderr, "\n");
+            }
             for (;;) {
                 if (++guard_words > (1ull << 34)) return -2; // runaway
                 const mk::DOp &I = D.at(pc);
@@ -93,6 +102,31 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
                     pc++;
                     break;
                 }
+                case mk::U_STX: {
+                    const int64_t x = reg(I.b);
+                    if (x < 0 || (uint64_t)I.imm + (uint64_t)x >= P.nslots) return -5; // index out of range
+                    slots[(uint32_t)(I.imm + x)] = (int32_t)sx(reg(I.a), ta);
+                    pc++;
+                    break;
+                }
+                case mk::U_LDX: {
+                    const int64_t x = reg(I.b);
+                    if (x < 0 || (uint64_t)I.imm + (uint64_t)x >= P.nslots) return -5;
+                    auto it = slots.find((uint32_t)(I.imm + x));
+                    if (it == slots.end()) return -3;
+                    reg(I.d) = it->second;
+                    pc++;
+                    break;
+                }
+                case mk::U_OVF:
+                    if ((uint64_t)reg(I.b) >= ((uint64_t)I.imm >> 32)) {
+                        steps += I.inc;
+                        outv = (I.fl & mk::UF_OUTREG) ? (int32_t)sx(reg(I.a), ta) : (int32_t)(uint32_t)(uint64_t)I.imm;
+                        st = I.d;
+                        done = leave = true;
+                    }
+                    pc++;
+                    break;
                 case mk::U_JUMP: steps += I.inc; sb = (uint32_t)I.imm; leave = true; break;
                 case mk::U_BR: {
                     const int64_t v = sx(reg(I.a), ta);

@@ -232,6 +232,9 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
             case U_LI: case U_LD: use(I.d); break;
             case U_ST: use(I.a); break;
             case U_STI: break;
+            case U_STX: use(I.a); use(I.b); break;
+            case U_LDX: use(I.d); use(I.b); break;
+            case U_OVF: if (I.fl & UF_OUTREG) use(I.a); use(I.b); break;
             case U_JUMP: ok = reach(v, (uint64_t)I.imm); leave = true; break;
             case U_BR:
                 use(I.a);
@@ -285,7 +288,7 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
         if (!g.seen[v]) continue;
         size_t lo = g.entry[v], hi = lo;
         if (g.D[lo].op == U_GUARD) ++lo, ++hi;
-        while (g.D[hi].op <= U_LD || g.D[hi].op == U_ROUND_END) ++hi;
+        while (body_op(g.D[hi].op)) ++hi;
         std::vector<const Run *> outer;
         g.runs[v] = find_runs(g.D, lo, hi, outer);
         if (counted[v]) g.ndops += (lo - g.entry[v]) + emitted_ops(g.runs[v], lo, hi) + 1;
@@ -370,8 +373,27 @@ struct OpWriter {
             e.line("    MK_SLOT_ST(slots, sstride, %s, (int32_t)%" PRId32 ");", slot, (int32_t)I.imm);
             return true;
         case U_LD: e.line("    %s%u = (int64_t)MK_SLOT_LD(slots, sstride, %s);", R, d, slot); return true;
+        // dynamic stacks: slot imm + index register (a per-lane slot number)
+        case U_STX:
+            e.line("    MK_SLOT_STX(slots, sstride, (uint32_t)(%uu + (uint32_t)%s), (int32_t)%s);", (uint32_t)I.imm,
+                   operand(I.b, false).c_str(), A.c_str());
+            return true;
+        case U_LDX:
+            e.line("    %s%u = (int64_t)MK_SLOT_LDX(slots, sstride, (uint32_t)(%uu + (uint32_t)%s));", R, d,
+                   (uint32_t)I.imm, operand(I.b, false).c_str());
+            return true;
         default: return false;
         }
+    }
+
+    // OVF: a PUSH onto a dynamic stack at its capacity ends the lane
+    std::string ovf_cond(const DOp &I) const { return "((uint64_t)" + operand(I.b, false) + " >= " + std::to_string((uint64_t)I.imm >> 32) + "ull)"; }
+    std::string ovf_result(const DOp &I) const
+    {
+        if (I.fl & UF_OUTREG) return "(int32_t)" + operand(I.a, I.fl & UF_TA);
+        char b[48];
+        snprintf(b, sizeof b, "(int32_t)%" PRId32, (int32_t)(uint32_t)(uint64_t)I.imm);
+        return b;
     }
 
     // t = IntClamp(ip + A, 0, len-1) with an int64 wrapping add (program.go:354,362)
@@ -402,7 +424,7 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
     std::vector<size_t> lds;
     for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
         const DOp &I = g.D[pc];
-        if (I.op == U_ST || I.op == U_STI) return false;
+        if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_OVF) return false;
         if (I.op == U_LD) lds.push_back(pc);
     }
     if (lds.empty()) return false;
@@ -501,7 +523,7 @@ void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs
         const DOp &I = g.D[pc];
         if (slot_op(I)) {
             w.data(I, expr(pc, advancing(I)).c_str());
-        } else if (I.op == U_ROUND_END) {
+        } else if (I.op == U_ROUND_END || I.op == U_OVF) { // in-line ends: the shape's callback
             round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str(), pc);
         } else {
             w.data(I);
@@ -643,13 +665,41 @@ void emit_budget_exit(Emitter &e, Emitter &tab, const RoundEnds &re, uint32_t v,
     e.line("    }");
 }
 
+// Whether [lo, hi) holds an OVF (a checked variant with one cannot use the
+// budget-exit lookup: a lane may end at the OVF before its round end).
+bool has_ovf(const Graph &g, size_t lo, size_t hi)
+{
+    for (size_t pc = lo; pc < hi; ++pc)
+        if (g.D[pc].op == U_OVF) return true;
+    return false;
+}
+
+// In-line ends of a body, in program order: OVF (capacity) and, in checked
+// variants that cannot use the lookup, ROUND_END (budget).  `L` prefixes the
+// lane state ("" or "L."), `fin` is the statement that leaves the lane.
+void emit_inline_end(const OpWriter &w, const DOp &I, const char *inc, const char *L, const char *fin)
+{
+    if (I.op == U_OVF) {
+        w.e.line("    if %s {", w.ovf_cond(I).c_str());
+        w.e.line("        %ssteps += %uu;", L, I.inc);
+        w.e.line("        %soutv = %s;", L, w.ovf_result(I).c_str());
+    } else {
+        w.e.line("    if ((uint64_t)%ssteps + %s >= (uint64_t)budget) {", L, inc);
+        w.e.line("        %ssteps += (uint32_t)%s;", L, inc);
+        w.e.line("        %soutv = %s;", L, w.result(I).c_str());
+    }
+    w.e.line("        %sst = %uu;", L, I.d);
+    w.e.line("        %s", fin);
+    w.e.line("    }");
+}
+
 // [lo, hi) of variant v's body: after its GUARD, up to its exit op.
 void body_range(const Graph &g, uint32_t v, size_t &lo, size_t &hi)
 {
     lo = g.entry[v];
     if (g.D[lo].op == U_GUARD) ++lo;
     hi = lo;
-    while (g.D[hi].op <= U_LD || g.D[hi].op == U_ROUND_END) ++hi;
+    while (body_op(g.D[hi].op)) ++hi;
 }
 
 // ---- stream shape: straight-line lane function ------------------------------
@@ -754,7 +804,8 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
         size_t lo, hi;
         body_range(g, v, lo, hi);
         const RoundEnds re = round_ends(g, v, lo, hi);
-        if (!re.segs.empty()) { // checked variant: always ends at a round end (emit_budget_exit)
+        const bool ovf = has_ovf(g, lo, hi);
+        if (!re.segs.empty() && !ovf) { // checked variant: always ends at a round end (emit_budget_exit)
             e.line("    {");
             e.line("    int32_t mk_o = 0;");
             emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
@@ -769,7 +820,8 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
             e.line("    }");
             continue;
         }
-        emit_body(w, g, v, lo, hi, [&](const DOp &, const char *, size_t) {});
+        emit_body(w, g, v, lo, hi,
+                  [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "", "goto done;"); });
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -849,6 +901,13 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("    __builtin_amdgcn_raw_buffer_store_b32((v), mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0)");
         e.line("#define MK_SLOT_LD(b, ss, s) \\");
         e.line("    ((int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), MK_SLOT_LANE, (int32_t)((uint32_t)(s) * 256u), 0))");
+        // a per-lane slot number goes into the vector offset
+        e.line("#undef MK_SLOT_STX");
+        e.line("#undef MK_SLOT_LDX");
+        e.line("#define MK_SLOT_STX(b, ss, s, v) \\");
+        e.line("    __builtin_amdgcn_raw_buffer_store_b32((v), mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (uint32_t)(s) * 256u), 0, 0)");
+        e.line("#define MK_SLOT_LDX(b, ss, s) \\");
+        e.line("    ((int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (uint32_t)(s) * 256u), 0, 0))");
         e.line("#endif");
     }
     if (checked) { // host tests only: the GPU kernel serves unguarded launches
@@ -873,6 +932,7 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
         const DOp &I = g.D[pc];
         switch (I.op) {
         case U_MOV: case U_LI: case U_ADD: case U_SUB: case U_ADDI: case U_RSUBI: case U_ST: case U_STI: case U_LD:
+        case U_STX: case U_LDX:
             continue;
         case U_JUMP:
             exit_pc = pc;
@@ -948,6 +1008,8 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         case U_ADD: case U_SUB: R(I.a); R(I.b); W(I.d); break;
         case U_LI: case U_LD: W(I.d); break;
         case U_ST: R(I.a); break;
+        case U_STX: R(I.a); R(I.b); break;
+        case U_LDX: R(I.b); W(I.d); break;
         default: break;
         }
     }
@@ -987,7 +1049,8 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         OpWriter n{e, w.p, "n"};
         for (size_t pc = gpc + 1; pc < xpc; ++pc) {
             const DOp &I = g.D[pc];
-            if (I.op == U_ST || I.op == U_STI) e.line("    if (a)");
+            // stores, and indexed loads (a lane that left may hold any index), only for lanes in the loop
+            if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_LDX) e.line("    if (a)");
             if (I.op == U_ADDI && (int)(I.d / 8) == ind) {
                 if (mode == LOOP_NARROW) {
                     if (I.imm == 1 || I.imm == -1) // x -/+ a: one subtract/add with the mask as carry
@@ -1195,7 +1258,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         size_t lo, hi;
         body_range(g, v, lo, hi);
         const RoundEnds re = round_ends(g, v, lo, hi);
-        if (!re.segs.empty()) { // checked variant: always ends at a round end (emit_budget_exit)
+        if (!re.segs.empty() && !has_ovf(g, lo, hi)) { // checked variant: always ends at a round end (emit_budget_exit)
             e.line("    int32_t mk_o = 0;");
             emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
                 if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
@@ -1211,7 +1274,9 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             e.line("    }");
             continue;
         }
-        emit_body(w, g, v, lo, hi, [&](const DOp &, const char *, size_t) {});
+        char fin[48];
+        snprintf(fin, sizeof fin, "L.sb = MK_SB_DONE; goto X%u;", v);
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "L.", fin); });
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -1885,6 +1950,9 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
         e.line("#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))");
         e.line("#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])");
     }
+    // per-lane slot numbers (dynamic stacks); the buffer-op form redefines them
+    e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
+    e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
     // vector out/status stores of the light stream kernel (MK_JIT_IO_NT=1: non-temporal, experiments)
     e.line("typedef int32_t mk_i32x4 __attribute__((ext_vector_type(4)));");
     if (lim.io_nt)

@@ -15,6 +15,7 @@
 #include "tis_sched.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <unordered_map>
@@ -52,7 +53,8 @@ struct Ctl {
     std::vector<uint16_t> ip;
     uint32_t pend = 0, hung = 0;
     uint64_t pfull = 0;
-    std::vector<uint32_t> depth;
+    std::vector<uint32_t> depth; // entries tracked symbolically (dynamic stacks: above the memory part)
+    std::vector<uint8_t> lo;     // dynamic stacks: known lower bound of the memory depth (0 or 1)
     bool in_avail = true;
     uint8_t out_cnt = 0;
     uint8_t pos = 0;
@@ -83,14 +85,21 @@ enum { A_CONT = 0, A_EXIT = 1 };
 
 class Compiler {
   public:
-    Compiler(const Network &net, uint32_t cap, bool soo, const SchedLimits &lim)
+    Compiler(const Network &net, uint32_t cap, bool soo, const SchedLimits &lim, const std::vector<uint8_t> &dyn)
         : net_(net), cap_(cap), soo_(soo), lim_(lim), N_(net.nprog), S_(net.uses_stacks ? net.nstack : 0)
     {
-        L0_ = 7 * N_ + 2;
+        L0_ = 7 * N_ + 2 + S_;
         home_.assign(L0_, -1);
+        dyn_base_.assign(S_, -1);
+        for (int s = 0; s < S_; s++)
+            if ((size_t)s < dyn.size() && dyn[s]) dyn_base_[s] = (int64_t)(ndyn_++) * cap_;
+        depths_seen_.assign(S_, {});
+        want_dyn_.assign(S_, 0);
     }
 
     bool run(SchedProgram &out, std::string &why);
+    // stacks whose depth should follow the data (set when the compile failed)
+    const std::vector<uint8_t> &want_dyn() const { return want_dyn_; }
 
   private:
     // ---- location space -------------------------------------------------
@@ -100,7 +109,8 @@ class Compiler {
     int PENDV(int n) const { return 6 * N_ + n; }
     int INL() const { return 7 * N_; }
     int OUTL() const { return 7 * N_ + 1; }
-    bool is32(int loc) const { return loc >= 2 * N_; }
+    int DEP(int s) const { return 7 * N_ + 2 + s; } // dynamic stack: entries in memory
+    bool is32(int loc) const { return loc >= 2 * N_ && loc < 7 * N_ + 2; }
 
     const Network &net_;
     uint32_t cap_;
@@ -138,14 +148,34 @@ class Compiler {
     bool any_slot_ = false;
     std::vector<std::vector<int32_t>> slot_id_; // [stack][depth] -> dense HBM slot, -1 = none yet
 
+    // Dynamic stacks.  A stack whose depth follows the data (a PUSH loop over
+    // an input-dependent count) would make the control state -- depths are
+    // part of it -- grow with the data.  Such a stack keeps its entries in a
+    // contiguous slot range [base, base + cap) instead: the depth of its
+    // memory part is a location (DEP: a constant 0, or a per-lane register),
+    // and only the entries pushed since the last superblock exit are tracked
+    // symbolically above it (ctl.depth = their number).  Every exit flushes
+    // them (STX at base + DEP + j, DEP += n).  PUSH checks the capacity in
+    // line (OVF); POP from an empty tracked part reads slot base + DEP - 1
+    // (LDX) once DEP >= 1 is known, which a branch on DEP == 0 establishes
+    // (taken: the stack is empty -- DEP becomes the constant 0 and the POP
+    // blocks; not taken: lo = 1).
+    std::vector<int64_t> dyn_base_; // first slot of a dynamic stack, -1 = ordinary stack
+    uint32_t ndyn_ = 0;
+    std::vector<std::unordered_set<uint32_t>> depths_seen_; // ordinary stacks: depths at superblock entries
+    std::vector<uint8_t> want_dyn_;
+
+    bool dyn(int s) const { return dyn_base_[s] >= 0; }
+
     uint32_t slot_of(int s, uint32_t d)
     {
+        any_slot_ = true;
+        if (dyn(s)) return (uint32_t)(dyn_base_[s] + d);
         if (slot_id_.size() < (size_t)S_) slot_id_.resize(S_);
         auto &v = slot_id_[s];
         if (v.size() <= d) v.resize(d + 1, -1);
         if (v[d] < 0) v[d] = (int32_t)max_slot_++;
-        any_slot_ = true;
-        return (uint32_t)v[d];
+        return (uint32_t)(ndyn_ * cap_ + v[d]);
     }
 
     // ---- helpers --------------------------------------------------------
@@ -212,7 +242,7 @@ class Compiler {
                 any = true;
                 Val &v = stk_[s][d];
                 if (v.kind == K_REG && refcnt_[v.r] == 1) {
-                    emit(U_ST, fa(v), 0, v.r, 0, slot_of(s, d));
+                    st_entry(s, d, v);
                     decref(v);
                     v = Val();
                     v.kind = K_MEM; // digest unchanged: still symbolic
@@ -234,6 +264,74 @@ class Compiler {
         code_.push_back(u);
     }
     void emit_ext(int64_t imm) { emit(0xFF, 0, 0, 0, 0, imm); }
+
+    // Store tracked entry d of stack s (value v: CONST or REG) to its slot:
+    // static for ordinary stacks and over a constant DEP, indexed by the DEP
+    // register otherwise.  Never allocates for a REG value (spill_one calls it).
+    void st_entry(int s, uint32_t d, const Val &v)
+    {
+        const Val &D = dyn(s) ? loc_[DEP(s)] : Val();
+        if (!dyn(s) || D.kind == K_CONST) {
+            const uint32_t slot = slot_of(s, (uint32_t)(dyn(s) ? D.c : 0) + d);
+            if (v.kind == K_CONST) emit(U_STI, 0, 0, slot & 0xFFFF, slot >> 16, v.c);
+            else emit(U_ST, fa(v), 0, v.r, 0, slot);
+            return;
+        }
+        any_slot_ = true;
+        int src = v.r;
+        uint8_t fl = fa(v);
+        if (v.kind == K_CONST) {
+            src = fresh_reg();
+            emit(U_LI, 0, src, 0, 0, v.c);
+            fl = 0;
+        }
+        emit(U_STX, fl, 0, src, D.r, dyn_base_[s] + d);
+    }
+    // Load tracked entry d (K_MEM) of stack s into register r.
+    void ld_entry(int s, uint32_t d, int r)
+    {
+        const Val &D = dyn(s) ? loc_[DEP(s)] : Val();
+        if (!dyn(s) || D.kind == K_CONST) {
+            emit(U_LD, 0, r, 0, 0, slot_of(s, (uint32_t)(dyn(s) ? D.c : 0) + d));
+            return;
+        }
+        any_slot_ = true;
+        emit(U_LDX, 0, r, 0, D.r, dyn_base_[s] + d);
+    }
+    // DEP(s) += k (dynamic stack), as a register.
+    void dep_add(int s, int64_t k)
+    {
+        const Val D = loc_[DEP(s)];
+        const int d = dest_for(DEP(s));
+        if (D.kind == K_CONST) emit(U_LI, 0, d, 0, 0, D.c + k);
+        else emit(U_ADDI, 0, d, D.r, 0, k);
+        Val nv;
+        nv.kind = K_REG;
+        nv.r = (uint16_t)d;
+        set_loc(DEP(s), nv);
+        r32_[d] = 0;
+    }
+    // At a superblock exit: every dynamic stack's tracked entries go to memory.
+    void flush_dyn()
+    {
+        for (int s = 0; s < S_; s++) {
+            if (!dyn(s) || stk_[s].empty()) continue;
+            const uint32_t n = (uint32_t)stk_[s].size();
+            for (uint32_t d = 0; d < n; d++) {
+                Val &v = stk_[s][d];
+                if (v.kind == K_CONST || v.kind == K_REG) st_entry(s, d, v);
+                decref(v);
+                v = Val();
+            }
+            const Val D = loc_[DEP(s)];
+            const int64_t lo = D.kind == K_CONST ? D.c + n : (int64_t)ctl_.lo[s] + n;
+            dep_add(s, n);
+            stk_[s].clear();
+            dig_[s] = StackDigest();
+            ctl_.depth[s] = 0;
+            ctl_.lo[s] = (uint8_t)std::min<int64_t>(lo, 1);
+        }
+    }
     uint8_t fa(const Val &v) const { return v.tr ? UF_TA : 0; }
     uint8_t fb(const Val &v) const { return v.tr ? UF_TB : 0; }
 
@@ -275,6 +373,8 @@ class Compiler {
     // ---- state management ---------------------------------------------
     void prune(Ctl &c, std::vector<Val> &loc) const;
     std::string key_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const;
+    std::string shape_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const;
+    std::unordered_map<std::string, uint32_t> shape_count_;
     uint32_t get_or_create(const Ctl &c, const std::vector<Val> &loc);
     void load_entry(uint32_t id);
 
@@ -282,11 +382,12 @@ class Compiler {
     // Moves every location that is symbolic in any successor into its home
     // register and stores symbolic stack entries.  `keep` is a value the
     // exit op still reads afterwards; returns where to read it.
-    Val canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep);
+    Val canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep);
     void exit_jump();
     void exit_end(uint8_t reason);
     void exit_branch(int n, uint8_t cond, uint16_t target);
     void exit_jro(int n, const Val &v);
+    void exit_pop_check(int s);
     void round_end_marker();
     void generalize();
 
@@ -367,6 +468,15 @@ void Compiler::prune(Ctl &c, std::vector<Val> &loc) const
     if (!c.in_avail) loc[INL()] = vdead();
 }
 
+// key_of without the constants' values (what widening compares)
+std::string Compiler::shape_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const
+{
+    std::vector<Val> l = loc;
+    for (int X = 0; X < 7 * N_ + 2; X++)
+        if (l[X].kind == K_CONST) l[X].c = 0;
+    return key_of(c, l, dig);
+}
+
 std::string Compiler::key_of(const Ctl &c, const std::vector<Val> &loc, const std::vector<StackDigest> &dig) const
 {
     std::string k;
@@ -377,6 +487,7 @@ std::string Compiler::key_of(const Ctl &c, const std::vector<Val> &loc, const st
     put(&c.hung, 4);
     put(&c.pfull, 8);
     put(c.depth.data(), c.depth.size() * 4);
+    put(c.lo.data(), c.lo.size());
     const uint8_t misc[4] = {(uint8_t)c.in_avail, c.out_cnt, c.pos, (uint8_t)c.changed};
     put(misc, 4);
     for (int X = 0; X < L0_; X++) {
@@ -397,7 +508,19 @@ uint32_t Compiler::get_or_create(const Ctl &c, const std::vector<Val> &loc)
     const std::string k = key_of(c, loc, dig_);
     auto it = memo_.find(k);
     if (it != memo_.end()) return it->second;
+    for (int s = 0; s < S_; s++) {
+        if (dyn(s)) continue;
+        auto &seen = depths_seen_[s];
+        seen.insert(c.depth[s]);
+        if (lim_.dyn_depths && seen.size() > lim_.dyn_depths) { // the depth follows the data
+            want_dyn_[s] = 1;
+            failf("stack depth follows the data");
+        }
+    }
+    if (fail_) return 0;
     if (entries_.size() >= lim_.max_superblocks) {
+        for (int s = 0; s < S_; s++)
+            if (!dyn(s) && lim_.dyn_depths && depths_seen_[s].size() > 1) want_dyn_[s] = 1;
         failf("superblock budget exceeded");
         return 0;
     }
@@ -425,6 +548,7 @@ uint32_t Compiler::get_or_create(const Ctl &c, const std::vector<Val> &loc)
     }
     e.dig = dig_;
     const uint32_t id = (uint32_t)entries_.size();
+    if (lim_.widen_after) shape_count_[shape_of(c, loc, dig_)]++;
     entries_.push_back(std::move(e));
     memo_.emplace(k, id);
     work_.push_back(id);
@@ -451,14 +575,33 @@ void Compiler::load_entry(uint32_t id)
     steps_ = 0;
 }
 
-Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep)
+Val Compiler::canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep)
 {
+    // 0. dynamic stacks: tracked entries to memory
+    for (int s = 0; s < S_; s++) {
+        if (!dyn(s) || stk_[s].empty()) continue;
+        flush_dyn();
+        for (Ctl &c : succ)
+            for (int t = 0; t < S_; t++)
+                if (dyn(t) && c.depth[t] != ctl_.depth[t]) c.depth[t] = ctl_.depth[t], c.lo[t] = ctl_.lo[t];
+        break;
+    }
     // 1. which locations must be in their home (symbolic in any successor)
     std::vector<uint8_t> need(L0_, 0);
     succ_loc.assign(succ.size(), loc_);
     for (size_t i = 0; i < succ.size(); i++) {
         Ctl c = succ[i];
         prune(c, succ_loc[i]);
+        // widening: a successor whose state differs from lim_.widen_after
+        // compiled states only in constants (a counter that changes every
+        // iteration of a loop on data) gets its constants as registers
+        if (lim_.widen_after && shape_count_[shape_of(c, succ_loc[i], dig_)] >= lim_.widen_after) {
+            for (int X = 0; X < 7 * N_ + 2; X++) {
+                if (succ_loc[i][X].kind != K_CONST) continue;
+                succ_loc[i][X].kind = K_REG;
+                need[X] = 1;
+            }
+        }
         for (int X = 0; X < L0_; X++)
             if (succ_loc[i][X].kind == K_REG || succ_loc[i][X].kind == K_MEM) need[X] = 1;
     }
@@ -467,7 +610,7 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
         for (uint32_t d = 0; d < (uint32_t)stk_[s].size(); d++) {
             Val &v = stk_[s][d];
             if (v.kind == K_REG) {
-                emit(U_ST, fa(v), 0, v.r, 0, slot_of(s, d));
+                st_entry(s, d, v);
                 decref(v);
                 v = Val();
                 v.kind = K_MEM;
@@ -503,6 +646,7 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
     // 4. parallel moves into homes
     struct Mv { int dst, src; bool tr; };
     std::vector<Mv> mv;
+    std::vector<std::pair<int, int64_t>> lis; // constants into homes, after the moves
     std::vector<uint8_t> isdst;
     for (int X = 0; X < L0_; X++) {
         if (!need[X]) continue;
@@ -510,7 +654,7 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
         const int h = home_[X];
         if (v.kind == K_CONST) {
             // constant in this trace but symbolic in a merged successor
-            emit(U_LI, 0, h, 0, 0, v.c);
+            lis.push_back({h, v.c});
             continue;
         }
         if (v.kind != K_REG) continue;
@@ -523,11 +667,18 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
         if ((size_t)m.dst >= isdst.size()) isdst.resize(m.dst + 1, 0);
         isdst[m.dst] = 1;
     }
-    // preserve `keep` if a move overwrites its register
+    for (auto &l : lis) {
+        ensure_reg(l.first);
+        if ((size_t)l.first >= isdst.size()) isdst.resize(l.first + 1, 0);
+        isdst[l.first] = 1;
+    }
+    // preserve `keep` if a move or a constant overwrites its register
     if (keep.kind == K_REG) {
         bool clobbered = false;
         for (auto &m : mv)
             if (m.dst == keep.r && !(m.src == keep.r && m.tr && keep.tr)) clobbered = true;
+        for (auto &l : lis)
+            if (l.first == keep.r) clobbered = true;
         if (clobbered) {
             std::vector<uint8_t> ex = isdst;
             for (auto &m : mv) {
@@ -556,10 +707,17 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
         if (progress) continue;
         // only cycles left: park one destination's current content in a temp
         const int d = mv[0].dst;
-        std::vector<uint8_t> ex(refcnt_.size() + 1, 0);
+        // not a register a move already wrote (a home whose new value is in
+        // place) nor a pending destination, source or the exit's operand
+        std::vector<uint8_t> ex = isdst;
+        if (ex.size() < refcnt_.size() + 1) ex.resize(refcnt_.size() + 1, 0);
         for (auto &m : mv) {
             if ((size_t)std::max(m.dst, m.src) >= ex.size()) ex.resize(std::max(m.dst, m.src) + 1, 0);
             ex[m.dst] = ex[m.src] = 1;
+        }
+        if (keep.kind == K_REG) { // the exit op still reads it (it may sit in a temp of its own)
+            if ((size_t)keep.r >= ex.size()) ex.resize(keep.r + 1, 0);
+            ex[keep.r] = 1;
         }
         const int t = fresh_reg(&ex);
         if (fail_) return keep;
@@ -567,6 +725,7 @@ Val Compiler::canonicalize(const std::vector<Ctl> &succ, std::vector<std::vector
         for (auto &m : mv)
             if (m.src == d) m.src = t;
     }
+    for (auto &l : lis) emit(U_LI, 0, l.first, 0, 0, l.second);
     if (keep.kind == K_REG) ensure_reg(keep.r);
     return keep;
 }
@@ -603,8 +762,8 @@ void Compiler::exit_branch(int n, uint8_t cond, uint16_t target)
     std::vector<std::vector<Val>> sl;
     const Val a = canonicalize(succ, sl, loc_[ACC(n)]);
     if (fail_) return;
-    const uint32_t it = get_or_create(t, sl[0]);
-    const uint32_t iff = get_or_create(f, sl[1]);
+    const uint32_t it = get_or_create(succ[0], sl[0]);
+    const uint32_t iff = get_or_create(succ[1], sl[1]);
     const int64_t imm = (int64_t)(((uint64_t)(2 * iff) << 32) | (uint64_t)(2 * it));
     emit(U_BR, (uint8_t)(fa(a) | (cond << UF_COND_SHIFT)), 0, a.r, 0, imm);
     emit_ext(steps_);
@@ -634,6 +793,25 @@ void Compiler::exit_jro(int n, const Val &v)
     emit_ext(steps_);
 }
 
+// POP from a dynamic stack whose memory part may be empty: branch on DEP.
+// Both successors re-attempt the POP (same node, same round position): the
+// taken one knows DEP == 0 (the constant: the POP blocks), the other DEP >= 1.
+void Compiler::exit_pop_check(int s)
+{
+    Ctl t = ctl_, f = ctl_;
+    f.lo[s] = 1;
+    std::vector<Ctl> succ{t, f};
+    std::vector<std::vector<Val>> sl;
+    const Val a = canonicalize(succ, sl, loc_[DEP(s)]);
+    if (fail_) return;
+    sl[0][DEP(s)] = vconst(0);
+    const uint32_t it = get_or_create(succ[0], sl[0]);
+    const uint32_t iff = get_or_create(succ[1], sl[1]);
+    const int64_t imm = (int64_t)(((uint64_t)(2 * iff) << 32) | (uint64_t)(2 * it));
+    emit(U_BR, (uint8_t)(fa(a) | (0 << UF_COND_SHIFT)), 0, a.r, 0, imm);
+    emit_ext(steps_);
+}
+
 void Compiler::round_end_marker()
 {
     const Val &o = loc_[OUTL()];
@@ -647,7 +825,7 @@ void Compiler::generalize()
 {
     // constants that keep changing (a loop over constant data) prevent the
     // state from ever repeating: turn every live constant into a register.
-    for (int X = 0; X < L0_; X++) {
+    for (int X = 0; X < 7 * N_ + 2; X++) { // not DEP: a constant DEP is 0 (empty)
         if (loc_[X].kind != K_CONST) continue;
         const int d = fresh_reg();
         emit(U_LI, 0, d, 0, 0, loc_[X].c);
@@ -661,8 +839,7 @@ void Compiler::generalize()
         for (uint32_t d = 0; d < (uint32_t)stk_[s].size(); d++) {
             Val &v = stk_[s][d];
             if (v.kind != K_CONST) continue;
-            const uint32_t slot = slot_of(s, d);
-            emit(U_STI, 0, 0, slot & 0xFFFF, slot >> 16, v.c);
+            st_entry(s, d, v);
             digest_entry(dig_[s], d, v, false);
             v = Val();
             v.kind = K_MEM;
@@ -718,13 +895,39 @@ int Compiler::attempt(int n)
         return A_CONT;
     case OP_POP: {
         const int s = I.arg;
-        if (ctl_.depth[s] == 0) return A_CONT;
+        if (ctl_.depth[s] == 0) {
+            if (!dyn(s)) return A_CONT; // empty: blocks
+            const Val D = loc_[DEP(s)];
+            if (D.kind == K_CONST && D.c == 0) return A_CONT;
+            if (D.kind == K_REG && ctl_.lo[s] == 0) {
+                exit_pop_check(s);
+                return A_EXIT;
+            }
+            // the memory part holds at least one entry: DEP -= 1, read slot DEP
+            if (D.kind == K_CONST) {
+                set_loc(DEP(s), vconst(D.c - 1));
+            } else {
+                dep_add(s, -1);
+                ctl_.lo[s]--;
+            }
+            if (I.dst) {
+                const int r = fresh_reg();
+                ld_entry(s, 0, r);
+                Val nv;
+                nv.kind = K_REG;
+                nv.r = (uint16_t)r;
+                set_loc(A, nv);
+                r32_[r] = 1;
+            }
+            retire();
+            return A_CONT;
+        }
         const uint32_t d = ctl_.depth[s] - 1;
         Val e = stk_[s][d];
         if (I.dst) {
             if (e.kind == K_MEM) {
                 const int r = fresh_reg();
-                emit(U_LD, 0, r, 0, 0, slot_of(s, d));
+                ld_entry(s, d, r);
                 Val nv;
                 nv.kind = K_REG;
                 nv.r = (uint16_t)r;
@@ -816,10 +1019,20 @@ int Compiler::attempt(int n)
         break;
     case OP_PUSH: {
         const int s = I.arg;
-        if (ctl_.depth[s] >= cap_) {
+        const Val D = dyn(s) ? loc_[DEP(s)] : vconst(0);
+        const int64_t known = (D.kind == K_CONST ? D.c : (int64_t)ctl_.lo[s]) + ctl_.depth[s];
+        if (known >= (int64_t)cap_) {
             exit_end(MK_ST_STACK_OVERFLOW);
             rc = A_EXIT;
             break;
+        }
+        if (D.kind == K_REG) { // the lane overflows here iff DEP >= cap - depth
+            const Val &o = loc_[OUTL()];
+            const uint8_t st = MK_ST_STACK_OVERFLOW | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+            const uint64_t lim = cap_ - ctl_.depth[s];
+            if (o.kind == K_REG) emit(U_OVF, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, D.r, 0);
+            else emit(U_OVF, 0, st, 0, D.r, o.kind == K_CONST ? o.c : 0);
+            emit_ext((int64_t)(((uint64_t)lim << 32) | steps_));
         }
         const Val e = trunc(v);
         incref(e);
@@ -898,8 +1111,10 @@ bool Compiler::run(SchedProgram &out, std::string &why)
     Ctl c;
     c.ip.assign(N_, 0);
     c.depth.assign(S_, 0);
+    c.lo.assign(S_, 0);
     ctl_ = c;
     loc_.assign(L0_, vdead());
+    for (int s = 0; s < S_; s++) loc_[DEP(s)] = vconst(0);
     for (int n = 0; n < N_; n++) {
         loc_[ACC(n)] = vconst(0);
         loc_[BAK(n)] = vconst(0);
@@ -936,7 +1151,7 @@ bool Compiler::run(SchedProgram &out, std::string &why)
             if (sc[i].op == U_ROUND_END) {
                 maxinc = std::max<int64_t>(maxinc, sc[i + 1].imm);
                 i++;
-            } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END) {
+            } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END || sc[i].op == U_OVF) {
                 i++;
             }
         }
@@ -962,7 +1177,8 @@ bool Compiler::run(SchedProgram &out, std::string &why)
     }
     out.jtab = jtab_;
     out.nregs = std::max<uint32_t>(max_reg_, 1);
-    out.nslots = any_slot_ ? max_slot_ : 0;
+    out.nslots = any_slot_ ? ndyn_ * cap_ + max_slot_ : 0;
+    out.ndyn = ndyn_;
     out.in_reg = 0;
     out.nsb = (uint32_t)entries_.size();
     out.sym_rounds = rounds_;
@@ -971,6 +1187,17 @@ bool Compiler::run(SchedProgram &out, std::string &why)
 
 } // namespace
 
+// MK_SCHED_WIDEN / MK_SCHED_DYN / MK_SCHED_MAX_SB override the widening
+// threshold, the dynamic-stack trigger and the superblock limit (experiments
+// and tests; unset = the caller's limits).
+SchedLimits lim_env(SchedLimits lim)
+{
+    if (const char *e = getenv("MK_SCHED_WIDEN")) lim.widen_after = (uint32_t)atoi(e);
+    if (const char *e = getenv("MK_SCHED_DYN")) lim.dyn_depths = (uint32_t)atoi(e);
+    if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
+    return lim;
+}
+
 bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
                       SchedProgram &out, std::string &why)
 {
@@ -978,8 +1205,19 @@ bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_outpu
         why = "network addresses remote peers (MK_NODE_REMOTE_*)";
         return false;
     }
-    Compiler c(net, stack_cap, stop_on_output, lim);
-    return c.run(out, why);
+    // A stack whose depth follows the data is found by compiling: the
+    // compile stops at the first such stack and is repeated with it dynamic.
+    const int S = net.uses_stacks ? net.nstack : 0;
+    std::vector<uint8_t> dyn(S, 0);
+    const SchedLimits L = lim_env(lim);
+    for (;;) {
+        Compiler c(net, stack_cap, stop_on_output, L, dyn);
+        if (c.run(out, why)) return true;
+        bool more = false;
+        for (int s = 0; s < S; s++)
+            if (c.want_dyn()[s] && !dyn[s]) dyn[s] = 1, more = true;
+        if (!more) return false;
+    }
 }
 
 std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std::vector<uint32_t> &entry_out)
@@ -994,7 +1232,7 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
         o.op = u.op;
         o.fl = u.fl;
         o.imm = u.imm;
-        const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END;
+        const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF;
         const uint32_t ext = two ? (uint32_t)p.code[i + 1].imm : 0;
         switch (u.op) {
         case U_MOV: case U_ADDI: case U_RSUBI:
@@ -1015,6 +1253,19 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
             o.d = u.d; o.a = u.a * scale; o.b = u.b; o.inc = ext; break;
         case U_END: case U_ROUND_END:
             o.d = u.d; o.a = (u.fl & UF_OUTREG) ? u.a * scale : 0; o.inc = ext; break;
+        case U_STX:
+            o.a = u.a * scale; o.b = u.b * scale; break;
+        case U_LDX:
+            o.d = u.d * scale; o.b = u.b * scale; break;
+        case U_OVF: {
+            const uint64_t x = (uint64_t)p.code[i + 1].imm;
+            o.d = u.d;
+            o.a = (u.fl & UF_OUTREG) ? u.a * scale : 0;
+            o.b = u.b * scale;
+            o.inc = (uint32_t)x;
+            o.imm = (int64_t)(((x >> 32) << 32) | (uint32_t)(int32_t)u.imm);
+            break;
+        }
         default: break;
         }
         out.push_back(o);
@@ -1028,8 +1279,8 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
 
 std::string sched_disasm(const SchedProgram &p)
 {
-    static const char *names[U_COUNT] = {"MOV", "LI", "ADD", "SUB", "ADDI", "RSUBI", "ST", "STI",
-                                         "LD", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END"};
+    static const char *names[U_COUNT] = {"MOV", "LI",  "ADD", "SUB", "ADDI",  "RSUBI",     "ST",  "STI", "LD",
+                                         "STX", "LDX", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END", "OVF"};
     std::string s;
     char buf[200];
     snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu\n", p.nsb, p.nregs, p.nslots,
@@ -1048,7 +1299,7 @@ std::string sched_disasm(const SchedProgram &p)
         snprintf(buf, sizeof buf, "  %5zu %-9s fl=%02x d=%u a=%u b=%u imm=%lld\n", i, nm, u.fl, u.d, u.a, u.b,
                  (long long)u.imm);
         s += buf;
-        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END) {
+        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF) {
             i++;
             snprintf(buf, sizeof buf, "        ext       steps+=%lld\n", (long long)p.code[i].imm);
             s += buf;

@@ -29,14 +29,22 @@ enum UOpCode : uint8_t {
     U_ST,       // slot[imm] = int32(A)
     U_STI,      // slot[a]   = int32(imm)
     U_LD,       // R[d] = sext32(slot[imm])
+    U_STX,      // slot[imm + R[b]] = int32(A)       (dynamic stack: R[b] = depth)
+    U_LDX,      // R[d] = sext32(slot[imm + R[b]])
     U_JUMP,     // steps += d | a<<16; sb = imm                                  (1 word)
     U_BR,       // steps += ext.imm; sb = cond(A) ? lo32(imm) : hi32(imm)         (2 words)
     U_JRO,      // steps += ext.imm; sb = jtab[imm + clamp(d + A, 0, b)]          (2 words)
     U_END,      // steps += ext.imm; out = OUTREG ? A : imm; status = d           (2 words)
     U_GUARD,    // if steps + (d | a<<16) >= budget: sb = imm (checked variant)   (1 word)
     U_ROUND_END,// if steps + ext.imm >= budget: END(status d, out A|imm)          (2 words)
+    U_OVF,      // if R[b] >= hi32(ext.imm): steps += lo32(ext.imm); END(status d, out A|imm)
+                // (a PUSH onto a dynamic stack at its capacity)                 (2 words)
     U_COUNT
 };
+
+constexpr uint8_t U_DATA_LAST = U_LDX; // ops <= this are data micro-ops
+// ops that may stand inside a superblock's body (data ops and in-line ends)
+inline bool body_op(uint32_t op) { return op <= U_DATA_LAST || op == U_ROUND_END || op == U_OVF; }
 
 // A = R[a] (sign-extended low 32 bits when UF_TA), B likewise with UF_TB.
 enum : uint8_t { UF_TA = 1, UF_TB = 2, UF_OUTREG = 4 };
@@ -61,6 +69,8 @@ struct SchedLimits {
     uint32_t soft_regs = 24;               // above this, spill stack entries to HBM first
     uint32_t idle_rounds = 64;             // rounds without emitted code before generalising
     uint64_t max_rounds = 1ull << 22;      // symbolic rounds in total (compile-time bound)
+    uint32_t dyn_depths = 24;              // distinct entry depths before a stack turns dynamic (0 = never)
+    uint32_t widen_after = 16;             // states of one shape with other constants before widening (0 = never)
 };
 
 struct SchedProgram {
@@ -69,6 +79,7 @@ struct SchedProgram {
     std::vector<uint32_t> jtab;  // JRO successor tables (variant ids)
     uint32_t nregs = 0;          // 64-bit registers per lane (LDS)
     uint32_t nslots = 0;         // stack memory slots per lane (HBM, lane-major)
+    uint32_t ndyn = 0;           // dynamic stacks (slots [k*cap, (k+1)*cap) each)
     uint32_t in_reg = 0;         // register holding the lane input at entry
     uint32_t nsb = 0;            // superblocks
     uint64_t sym_rounds = 0;     // rounds executed symbolically
@@ -85,6 +96,9 @@ struct SchedProgram {
 //   BR: a = cond offset, imm = lo:taken hi:not-taken, inc = steps
 //   JRO: d = ip, a = operand offset, b = len-1, imm = jtab offset, inc = steps
 //   END/ROUND_END: d = status, a = out offset (UF_OUTREG) else imm, inc = steps
+//   STX: a = src offset, b = index offset, imm = base slot   LDX: d, b, imm likewise
+//   OVF: d = status, a = out offset (UF_OUTREG), b = depth offset, inc = steps,
+//        imm = (uint32_t)out value | (uint64_t)limit << 32
 struct DOp {
     uint32_t op, fl, d, a, b, inc;
     int64_t imm;

@@ -10,7 +10,7 @@ import pytest
 import misaka_net_amd as mk
 from misaka_net_amd import _native as N
 from oracle import pyoracle as po
-from tisgen import loop_cases, random_network
+from tisgen import loop_cases, random_network, stack_loop_network
 
 pytestmark = pytest.mark.gpu
 
@@ -215,6 +215,39 @@ def test_random_networks_bit_exact(gpu, seed, mode):
         plan = net.plan(stack_cap=kw["stack_cap"], stop_on_output=kw["stop_on_output"])
         assert plan.startswith(("tier=native", "tier=interp")) or " native=" in plan, plan
     assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
+
+
+# Stack depths that follow the data (the schedule compiler's dynamic stacks:
+# STX/LDX at base + depth register, in-line OVF, the empty-check branch):
+# tisgen.stack_loop_network on every tier, capacities and budgets that end
+# lanes inside pushes and pops (stack.go:95-155, program.go:475-566).
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("seed", range(0, 60))
+def test_dynamic_stack_networks_bit_exact(gpu, seed, mode):
+    rows, gen = stack_loop_network(seed)
+    xs = po.gen_inputs(seed + 5, 2048, **gen)
+    kw = dict(budget=[None, 57, 300, 2000][seed % 4], stack_cap=[None, 3, 17, 64, 200][seed % 5])
+    kw = {k: v for k, v in kw.items() if v is not None}
+    got = mk.Network(rows).compute_batch(xs, mode=_m(mode), **kw)
+    assert_same(got, oracle(rows, xs, **kw), f"seed {seed}")
+
+
+# The census classes whose depths follow the data, at their bench size
+# (1,048,576 lanes, inputs 0..255) on the default path, now the native tier:
+# every lane exact against an oracle table over all 256 inputs.
+@pytest.mark.parametrize("cls", ["data_dependent_stack_depth", "two_stacks_independent_depths"])
+@pytest.mark.parametrize("mode", ["auto", "tile"])
+def test_dynamic_stack_census_full_size(gpu, cls, mode):
+    n = 1 << 20
+    nodes = mk.networks.census_classes()[cls][0][1]
+    net = mk.Network(nodes)
+    if mode == "auto":
+        assert net.plan().startswith("tier=native"), net.plan()
+    out, st, sp, stats = _device_run(net, n, gen=(N.MK_GEN_MASKED, 255), mode=_m(mode))
+    x = po.gen_inputs(SEED, n, kind=N.MK_GEN_MASKED, mask=255)
+    t_out, t_st, t_sp = oracle(nodes, np.arange(256, dtype=np.int64))
+    assert np.array_equal(out, t_out[x]) and np.array_equal(st, t_st[x]) and np.array_equal(sp, t_sp[x])
+    assert stats[0] == int(sp.astype(np.int64).sum()) and stats[2] == n
 
 
 @pytest.mark.parametrize("mode", MODES)

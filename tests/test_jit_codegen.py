@@ -16,7 +16,7 @@ import pytest
 import misaka_net_amd as mk
 from oracle import pyoracle as po
 import schedcheck as sc
-from tisgen import loop_cases, random_network
+from tisgen import census_classes, stack_loop_network, loop_cases, random_network
 
 SEED = 0x4D49534B41
 
@@ -30,6 +30,8 @@ HEADER = """#include <cstdint>
 #define MK_ALL(p) (p)
 #define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))
 #define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])
+#define MK_SLOT_STX(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))
+#define MK_SLOT_LDX(b, ss, s) ((b)[(uint64_t)(s) * (ss)])
 #define MK_FLAG_GT(x) ((int32_t)((x) > 0))
 #define MK_FLAG_LT(x) ((int32_t)((x) < 0))
 #define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
@@ -143,6 +145,26 @@ def test_random_networks(tmp_path, block, machine):
     assert len(check_cases(tmp_path, cases, machine)) >= 30
 
 
+@pytest.mark.parametrize("machine", [False, True])
+@pytest.mark.parametrize("block", range(3))
+def test_dynamic_stack_networks(tmp_path, block, machine):
+    # stack depths that follow the data (tisgen.stack_loop_network): dynamic
+    # stacks (STX/LDX, in-line OVF, the empty-check branch), capacities and
+    # budgets that end lanes inside pushes and pops
+    cases = []
+    for seed in range(block * 30, block * 30 + 30):
+        rows, gen = stack_loop_network(seed)
+        kw = dict(budget=[None, 57, 300, 2000][seed % 4], stack_cap=[None, 3, 17, 64, 200][seed % 5])
+        kw = {k: v for k, v in kw.items() if v is not None}
+        cases.append((f"seed{seed}", rows, po.gen_inputs(seed + 5, 96, **gen), kw))
+    for cls in ("data_dependent_stack_depth", "two_stacks_independent_depths"):
+        nodes = census_classes()[cls][0][1]
+        for cap in (None, 5, 200):
+            xs = po.gen_inputs(3, 256, kind=1, mask=255)
+            cases.append((f"{cls}_{cap}", nodes, xs, {"stack_cap": cap} if cap else {}))
+    assert len(check_cases(tmp_path, cases, machine)) >= 24
+
+
 def test_shapes():
     # acyclic schedules stream; data-dependent loops get the machine shape
     assert sc.jit_lane(mk.networks.example_network(), with_shape=True)[2] == "stream"
@@ -196,6 +218,22 @@ def test_compile_bounds_fall_back_with_reason(monkeypatch):
     monkeypatch.setenv("MK_JIT_COMPILE_S", "0.001")
     plan = mk.Network(mk.networks.pipeline_network(256)).plan()
     assert plan.startswith("tier=compiled ") and "did not finish" in plan, plan
+
+
+@pytest.mark.parametrize("cls", ["data_dependent_stack_depth", "two_stacks_independent_depths"])
+@pytest.mark.parametrize("heavy", [False, True])
+def test_dynamic_stack_module_compiles_for_gfx950(cls, heavy, monkeypatch):
+    # the census classes whose stack depths follow the data run natively
+    # (machine shape; forced stream + heavy: the buffer-op form of the
+    # per-lane slot numbers, MK_SLOT_STX/LDX)
+    if heavy:
+        monkeypatch.setenv("MK_JIT_SHAPE", "stream")
+        monkeypatch.setenv("MK_JIT_HEAVY_OPS", "1")
+    net = mk.Network(mk.networks.census_classes()[cls][0][1])
+    plan = net.plan(mode="jit")
+    assert plan.startswith("tier=native "), plan
+    src = net.jit_source()
+    assert "MK_SLOT_STX" in src and "MK_SLOT_LDX" in src
 
 
 def test_knobs_are_snapshotted_per_network(monkeypatch):

@@ -8,7 +8,7 @@ import pytest
 import misaka_net_amd as mk
 from oracle import pyoracle as po
 import schedcheck as sc
-from tisgen import random_network
+from tisgen import random_network, stack_loop_network
 
 SEED = 0x4D49534B41
 
@@ -75,3 +75,28 @@ def test_wide_immediates_on_symbolic_acc():
             "ADD 9223372036854775807\nSUB -9223372036854775808\nMOV ACC, n:R1\nMOV R1, ACC\n"
             "JRO 2147483648\nNOP\nOUT ACC\nJLZ L\nOUT 1\nL: OUT 2")
     same([("n", "program", prog)], po.gen_inputs(SEED, 500))
+
+
+def test_dynamic_stack_networks():
+    # stack depths that follow the data: the compiler's dynamic stacks
+    # (tisgen.stack_loop_network), host model vs oracle over capacities and
+    # budgets; every one of them compiles now
+    for seed in range(300):
+        rows, gen = stack_loop_network(seed)
+        xs = po.gen_inputs(seed + 5, 64, **gen)
+        for cap, budget in ((None, None), (3, 200), (17, 1000), (64, 57)):
+            kw = {k: v for k, v in (("stack_cap", cap), ("budget", budget)) if v is not None}
+            same(rows, xs, **kw)
+
+
+def test_exit_moves_keep_the_branch_operand():
+    # regressions of canonicalize: a SWP-driven swap of two homes (a move
+    # cycle) at a branch on ACC, and a cycle temp that took a home written by
+    # an earlier move of the same exit
+    a = "IN ACC\nL0: PUSH 4, s0\nSUB 2\nJGZ L0\nL1: SWP\nSWP\nSWP\nPUSH ACC, s1\nPOP s0, ACC\nSWP\nJGZ L1"
+    rows = [("b", "program", "C: POP s0, ACC\nADD 1\nSWP\nJMP C"), ("s0", "stack", ""), ("s1", "stack", ""),
+            ("a", "program", a)]
+    same(rows, np.arange(0, 64))
+    a = "IN ACC\nSAV\nL2: NOP\nPUSH ACC, s0\nSWP\nSUB 1\nJGZ L2\nPUSH -1, s0\nMOV R0, ACC\nOUT ACC"
+    b = "C: POP s0, ACC\nJLZ E\nSWP\nADD 1\nSWP\nJMP C\nE: SWP\nMOV ACC, a:R0"
+    same([("s0", "stack", ""), ("a", "program", a), ("b", "program", b)], np.arange(0, 80))

@@ -204,3 +204,51 @@ def loop_cases(n: int = 512, seed: int = 7):
 
 # ---- census classes: network shapes that stress the schedule compiler -----------
 from misaka_net_amd.networks import census_classes  # noqa: E402,F401  (defined with the bench workloads)
+
+
+def stack_loop_network(seed: int):
+    """Networks whose stack depths follow the data (the schedule compiler's
+    dynamic stacks): loops with input-dependent trip counts that push and pop
+    on 1-3 stacks, pops that may outnumber pushes (the POP then blocks), a
+    second node popping what the first pushes (cross-node blocking), and
+    values that reach the output (sums of popped values).  Returns
+    (rows, gen kwargs for oracle.gen_inputs)."""
+    r = random.Random(seed)
+    ns = r.randint(1, 3)
+    stacks = [f"s{k}" for k in range(ns)]
+    lines = ["IN ACC"]
+    if r.random() < 0.5:
+        lines.append(f"ADD {r.randint(-3, 3)}")
+    lines.append("SAV")
+    consumer = r.random() < 0.35
+    for k in range(r.randint(1, 3)):
+        s = r.choice(stacks)
+        lab = f"L{k}"
+        body = []
+        for _ in range(r.randint(1, 3)):
+            c = r.random()
+            if c < 0.45:
+                body.append(f"PUSH ACC, {r.choice(stacks)}")
+            elif c < 0.6:
+                body.append(f"PUSH {r.randint(-5, 5)}, {r.choice(stacks)}")
+            elif c < 0.8 and not consumer:
+                body.append(f"POP {r.choice(stacks)}, NIL")
+            else:
+                # accumulate a popped value into BAK (ACC is the counter)
+                body += ["SWP", f"PUSH ACC, {s}", f"POP {r.choice(stacks)}, ACC", "SWP"]
+        step = r.choice([1, 1, 2, 3])
+        jump = r.choice(["JGZ", "JGZ", "JNZ"]) if step == 1 else "JGZ"
+        lines += [f"{lab}: " + body[0]] + body[1:] + [f"SUB {step}", f"{jump} {lab}"]
+        if r.random() < 0.5:
+            lines += ["SWP", "SAV"]  # the next loop counts from the running value
+    if consumer:
+        lines += [f"PUSH -1, {stacks[0]}", "MOV R0, ACC", "OUT ACC"]
+        cons = (f"MOV 0, ACC\nSAV\nC: POP {stacks[0]}, ACC\nJLZ E\nSWP\nADD 1\nSWP\nJMP C\n"
+                f"E: SWP\nMOV ACC, a:R0")
+        rows = [("a", "program", "\n".join(lines)), ("b", "program", cons)]
+    else:
+        tail = r.choice(["SWP\nOUT ACC", "OUT ACC", f"POP {stacks[-1]}, ACC\nOUT ACC", "MOV 9, ACC\nOUT ACC"])
+        rows = [("a", "program", "\n".join(lines) + "\n" + tail)]
+    rows += [(s, "stack", "") for s in stacks]
+    r.shuffle(rows)
+    return rows, dict(kind=1, mask=r.choice([15, 63, 255]))
