@@ -932,7 +932,7 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
         const DOp &I = g.D[pc];
         switch (I.op) {
         case U_MOV: case U_LI: case U_ADD: case U_SUB: case U_ADDI: case U_RSUBI: case U_ST: case U_STI: case U_LD:
-        case U_STX: case U_LDX:
+        case U_STX: case U_LDX: case U_OVF:
             continue;
         case U_JUMP:
             exit_pc = pc;
@@ -1010,13 +1010,21 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         case U_ST: R(I.a); break;
         case U_STX: R(I.a); R(I.b); break;
         case U_LDX: R(I.b); W(I.d); break;
+        case U_OVF: R(I.b); if (I.fl & UF_OUTREG) R(I.a); break;
         default: break;
         }
     }
+    // A PUSH onto a dynamic stack in the body (OVF): a lane at the capacity
+    // leaves the loop there -- its flag drops, the iteration's register writes
+    // are discarded by the selects and its steps stop at the iteration's
+    // start; the OVF's step count, status and output are recorded and applied
+    // after the loop.  Trip counts then come from the per-lane counter.
+    bool ovf = false;
+    for (size_t pc = gpc + 1; pc < xpc; ++pc) ovf = ovf || g.D[pc].op == U_OVF;
     // induction register: written once per iteration, by r += imm (no truncation)
     int ind = -1;
     int64_t step = 0;
-    for (size_t pc = gpc + 1; pc < xpc && ind < 0; ++pc) {
+    for (size_t pc = gpc + 1; pc < xpc && ind < 0 && !ovf; ++pc) {
         const DOp &I = g.D[pc];
         if (I.op == U_ADDI && I.a == I.d && !(I.fl & UF_TA) && nwr[I.d / 8] == 1 && I.imm != 0 &&
             I.imm > -(int64_t(1) << 31) && I.imm < (int64_t(1) << 31))
@@ -1028,7 +1036,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     // exit condition on a register that only changes when the lane is active
     // (the induction register, or one the body never writes) stays false:
     // there `a` is the condition itself, one compare and no mask AND.
-    const bool cond_is_flag = X.op == U_BR && ((int)(X.a / 8) == ind || !wr[X.a / 8]);
+    const bool cond_is_flag = !ovf && X.op == U_BR && ((int)(X.a / 8) == ind || !wr[X.a / 8]);
     if (X.op == U_BR) {
         R(X.a);
         const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
@@ -1051,7 +1059,13 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             const DOp &I = g.D[pc];
             // stores, and indexed loads (a lane that left may hold any index), only for lanes in the loop
             if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_LDX) e.line("    if (a)");
-            if (I.op == U_ADDI && (int)(I.d / 8) == ind) {
+            if (I.op == U_OVF) {
+                e.line("    {");
+                e.line("    const bool o_ = a && %s;", n.ovf_cond(I).c_str());
+                e.line("    if (o_) { ovf_ = true; ovs_ = %uu; ovst_ = %uu; ovo_ = %s; }", I.inc, I.d, n.ovf_result(I).c_str());
+                e.line("    a = a && !o_;");
+                e.line("    }");
+            } else if (I.op == U_ADDI && (int)(I.d / 8) == ind) {
                 if (mode == LOOP_NARROW) {
                     if (I.imm == 1 || I.imm == -1) // x -/+ a: one subtract/add with the mask as carry
                         e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)a);", I.imm < 0 ? '-' : '+');
@@ -1101,6 +1115,11 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    }");
     e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
     e.line("    bool a = true, more = true;");
+    if (ovf) {
+        e.line("    bool ovf_ = false;");
+        e.line("    uint32_t ovs_ = 0u, ovst_ = 0u;");
+        e.line("    int32_t ovo_ = 0;");
+    }
     e.line("    {");
     e.line("    const uint32_t s0 = L.steps;");
     if (ind >= 0) e.line("    const int64_t i0 = L.r%d;", ind);
@@ -1153,6 +1172,15 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    }");
     // a: still in the loop (suspended); otherwise it left through the branch
     // (the condition on its frozen registers fails) or through the guard
+    if (ovf) {
+        e.line("    if (ovf_) {");
+        e.line("        L.steps += ovs_;");
+        e.line("        L.st = ovst_;");
+        e.line("        L.outv = ovo_;");
+        e.line("        L.sb = MK_SB_DONE;");
+        e.line("        break;");
+        e.line("    }");
+    }
     OpWriter l{e, w.p, "L.r"};
     std::string cl = "true";
     if (X.op == U_BR) {
