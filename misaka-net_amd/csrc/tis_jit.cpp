@@ -1587,6 +1587,148 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 }
 )";
 
+// Kernel of the machine shape with lanes grouped by value inside a tile.
+// A block takes tiles of MK_TS_T = 1024 contiguous inputs (grid-stride):
+//   1. loads them (coalesced) and buckets them by value in LDS: block
+//      min / max, 256 buckets of equal width (a power of two), an LDS
+//      histogram, its prefix sum and a scatter -- a counting sort whose
+//      order inside a bucket does not matter;
+//   2. runs them in sorted order, 64 at a time per wave (four rounds, the
+//      waves' chunks in snake order so that each wave's four chunks
+//      balance), every chunk by generations (mk_run on the superblock of the
+//      lowest running lane until every lane of the chunk has ended);
+//   3. writes the tile's out / status / steps back through LDS, coalesced.
+// Equal inputs take identical paths, and where trip counts follow the input
+// (C5's countdowns, the census classes' push loops) a chunk's lanes leave
+// their loops together: the idle lanes of generations over unsorted inputs
+// (a wave runs each loop for its longest trip) mostly go away, without the
+// global sort's atomics and scattered result writes (MK_JIT_ORDER).
+static const char *const kMachineSortKernel = R"(
+#define MK_TS_R 4u
+#define MK_TS_T (256u * MK_TS_R)
+#define MK_TS_NB 256u
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    __shared__ int32_t s_key[MK_TS_T];
+    __shared__ int32_t s_out[MK_TS_T];
+    __shared__ uint32_t s_steps[MK_TS_T];
+    __shared__ uint16_t s_pos[MK_TS_T];
+    __shared__ uint8_t s_st[MK_TS_T];
+    __shared__ uint32_t s_cnt[MK_TS_NB];
+    __shared__ uint32_t s_red[8];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
+    const uint32_t pol = MK_POLICY;
+    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    const uint64_t ntiles = (p.n + MK_TS_T - 1) / MK_TS_T;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * MK_TS_T;
+        const uint32_t m = p.n - base < MK_TS_T ? (uint32_t)(p.n - base) : MK_TS_T;
+        const bool vec = p.io_vec && m == MK_TS_T;
+        // 1. inputs 4 tid .. 4 tid + 3 of the tile, their range
+        int32_t v[4];
+        if (vec) {
+            const int4 q = *reinterpret_cast<const int4 *>((const int32_t *)p.in_data + base + 4u * tid);
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
+            for (uint32_t k = 0; k < 4u; ++k) v[k] = 4u * tid + k < m ? sched_input(p, base + 4u * tid + k) : 0;
+        }
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u; // biased: signed order as unsigned
+        for (uint32_t k = 0; k < 4u; ++k) {
+            if (4u * tid + k >= m) continue;
+            const uint32_t b = (uint32_t)v[k] ^ 0x80000000u;
+            lo = b < lo ? b : lo;
+            hi = b > hi ? b : hi;
+        }
+        s_cnt[tid] = 0u;
+        lo = MK_WAVE_MIN(lo);
+        hi = MK_WAVE_MAX(hi);
+        if (lane == 0u) {
+            s_red[wave] = lo;
+            s_red[4u + wave] = hi;
+        }
+        __syncthreads();
+        for (uint32_t w = 0; w < 4u; ++w) {
+            lo = s_red[w] < lo ? s_red[w] : lo;
+            hi = s_red[4u + w] > hi ? s_red[4u + w] : hi;
+        }
+        // bucket = (x - lo) >> sh, sh the smallest shift that fits the range into 256 buckets
+        const uint32_t span = hi - lo;
+        const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
+        const uint32_t sh = bits > 8u ? bits - 8u : 0u;
+        uint32_t bk[4];
+        for (uint32_t k = 0; k < 4u; ++k) {
+            bk[k] = (((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh;
+            if (4u * tid + k < m) atomicAdd(&s_cnt[bk[k]], 1u);
+        }
+        __syncthreads();
+        // exclusive prefix sum over the 256 buckets (thread tid owns bucket tid)
+        {
+            const uint32_t c = s_cnt[tid];
+            uint32_t x = c;
+            for (uint32_t o = 1u; o < 64u; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63u) s_red[wave] = x;
+            __syncthreads();
+            uint32_t pre = 0u;
+            for (uint32_t w = 0; w < wave; ++w) pre += s_red[w];
+            s_cnt[tid] = pre + x - c;
+            __syncthreads();
+        }
+        for (uint32_t k = 0; k < 4u; ++k) {
+            if (4u * tid + k >= m) continue;
+            const uint32_t d = atomicAdd(&s_cnt[bk[k]], 1u);
+            s_key[d] = v[k];
+            s_pos[d] = (uint16_t)(4u * tid + k);
+        }
+        __syncthreads();
+        // 2. the sorted lanes, 64 per wave and round
+        for (uint32_t r = 0; r < MK_TS_R; ++r) {
+            const uint32_t c = r * 4u + ((r & 1u) ? 3u - wave : wave);
+            const uint32_t j = c * 64u + lane;
+            const bool live = j < m;
+            MkLane L;
+            mk_init(L, live ? s_key[j] : 0);
+            if (!live) L.sb = MK_SB_IDLE;
+            for (;;) {
+                const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
+                if (!actb) break;
+                const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
+                const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
+                if (L.sb == u) mk_run(u, L, p.budget, slots, p.lanes, pol, smax);
+            }
+            if (live) {
+                const uint32_t at = s_pos[j];
+                s_out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+                s_st[at] = (uint8_t)L.st;
+                s_steps[at] = L.steps;
+                count_lane(cnt, L.steps, L.st);
+            }
+        }
+        __syncthreads();
+        // 3. results of the tile, in input order
+        if (vec) {
+            const uint32_t i = 4u * tid;
+            MK_IO_ST(reinterpret_cast<mk_i32x4 *>(p.out + base + i), (mk_i32x4{s_out[i], s_out[i + 1], s_out[i + 2], s_out[i + 3]}));
+            MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base + i),
+                     (uint32_t)s_st[i] | (uint32_t)s_st[i + 1] << 8 | (uint32_t)s_st[i + 2] << 16 | (uint32_t)s_st[i + 3] << 24);
+            if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base + i) = make_uint4(s_steps[i], s_steps[i + 1], s_steps[i + 2], s_steps[i + 3]);
+        } else {
+            for (uint32_t i = tid; i < m; i += 256u) {
+                p.out[base + i] = s_out[i];
+                p.status[base + i] = s_st[i];
+                if (p.steps) p.steps[base + i] = s_steps[i];
+            }
+        }
+        __syncthreads(); // the next tile reuses the LDS arrays
+    }
+    if (p.partials) write_partials(p.partials, gid, cnt);
+}
+)";
+
 JitLimits JitLimits::from_env()
 {
     JitLimits l;
@@ -1622,6 +1764,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_IO_NT", l.io_nt);
     num("MK_JIT_POOL", l.pool);
     flag("MK_JIT_ORDER", l.order);
+    flag("MK_JIT_TILE_SORT", l.tile_sort);
     return l;
 }
 
@@ -1629,9 +1772,11 @@ std::string JitLimits::key() const
 {
     char b[256];
     snprintf(b, sizeof b,
-             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d",
+             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
+             "tsort=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
-             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order);
+             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
+             (int)tile_sort);
     return b;
 }
 
@@ -2010,7 +2155,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.s += kDeviceCommon;
     e.s += "\n";
     e.s += lane_src;
-    const char *mk = kMachineKernel;
+    const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
     else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;
     e.s += shape == JIT_MACHINE ? mk : heavy ? kStreamKernelHeavy : kStreamKernel;

@@ -83,6 +83,10 @@ struct JitLimits {
     // sort's contended bucket atomics and the scattered result writes cost
     // more than the idle lanes it saves (780 vs 367 us, r02g).
     bool order = false;
+    // Machine shape: group the inputs by value inside each block's tile of
+    // 1024 (an LDS counting sort, kMachineSortKernel) so that a wave's lanes
+    // have similar loop trip counts (MK_JIT_TILE_SORT=0: input order).
+    bool tile_sort = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
