@@ -1205,6 +1205,11 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("#endif");
     e.line("#define MK_SB_DONE 0xFFFFFFFEu");
     e.line("#define MK_SB_IDLE 0xFFFFFFFFu");
+    {
+        uint32_t used = 0;
+        for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1u : 0u;
+        e.line("#define MK_LANE_REGS %uu", used); // 64-bit lane registers (kMachineSortKernel's occupancy)
+    }
     e.line("struct MkLane {");
     for (uint32_t r = 0; r < p.nregs; ++r)
         if (g.used_reg[r]) e.line("    int64_t r%u;", r);
@@ -1607,7 +1612,14 @@ static const char *const kMachineSortKernel = R"(
 #define MK_TS_R 4u
 #define MK_TS_T (256u * MK_TS_R)
 #define MK_TS_NB 256u
-extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+// MK_JIT_TS_WAVES asks the allocator for that many waves per SIMD on small
+// lane states (C5 at 8: 79 -> 63 VGPRs, yet 220 vs 215 us: off by default).
+#if MK_LANE_REGS <= 8 && MK_TS_WAVES_N
+#define MK_TS_WAVES __attribute__((amdgpu_waves_per_eu(MK_TS_WAVES_N)))
+#else
+#define MK_TS_WAVES
+#endif
+extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParams p)
 {
     __shared__ int32_t s_key[MK_TS_T];
     __shared__ int32_t s_out[MK_TS_T];
@@ -1619,7 +1631,9 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
     const uint32_t pol = MK_POLICY;
-    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    // counters, wave-uniform (scalar registers): steps, outputs, lanes, and the four end reasons
+    uint64_t c_steps = 0u;
+    uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
     const uint64_t ntiles = (p.n + MK_TS_T - 1) / MK_TS_T;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1705,8 +1719,16 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
                 s_out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
                 s_st[at] = (uint8_t)L.st;
                 s_steps[at] = L.steps;
-                count_lane(cnt, L.steps, L.st);
             }
+            const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
+            c_steps += (uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps & 0xffffu) : 0u)) +
+                       ((uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps >> 16) : 0u)) << 16);
+            c_out += (uint32_t)__popcll(__ballot(live && (L.st & MK_ST_HAS_OUTPUT)));
+            c_done += (uint32_t)__popcll(__ballot(live));
+            c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
+            c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
+            c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
+            c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
         }
         __syncthreads();
         // 3. results of the tile, in input order
@@ -1725,7 +1747,16 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
         }
         __syncthreads(); // the next tile reuses the LDS arrays
     }
-    if (p.partials) write_partials(p.partials, gid, cnt);
+    if (p.partials && lane == 0u) { // this wave's row (write_partials' layout)
+        unsigned long long *q = p.partials + (gid >> 6) * 8u;
+        q[0] += c_steps;
+        q[1] += c_out;
+        q[2] += c_done;
+        q[3] += c_qu;
+        q[4] += c_bu;
+        q[5] += c_ov;
+        q[6] += c_os;
+    }
 }
 )";
 
@@ -1765,6 +1796,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_POOL", l.pool);
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
+    num("MK_JIT_TS_WAVES", l.ts_waves);
     return l;
 }
 
@@ -1773,10 +1805,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d",
+             "tsort=%d,tsw=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort);
+             (int)tile_sort, ts_waves);
     return b;
 }
 
@@ -2099,6 +2131,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // machine-shape policy word, a constant of the module so that the loop
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
+    e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks

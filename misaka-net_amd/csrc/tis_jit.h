@@ -87,6 +87,10 @@ struct JitLimits {
     // 1024 (an LDS counting sort, kMachineSortKernel) so that a wave's lanes
     // have similar loop trip counts (MK_JIT_TILE_SORT=0: input order).
     bool tile_sort = true;
+    // Its occupancy target for small lane states (waves per SIMD handed to
+    // the register allocator, MK_JIT_TS_WAVES; 0: the compiler's choice --
+    // measured best: C5 215 us vs 220 at 8 and 243 at 6, r02l).
+    uint32_t ts_waves = 0;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
