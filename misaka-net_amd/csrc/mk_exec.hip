@@ -596,8 +596,34 @@ __device__ __forceinline__ bool apply_ovf(const DOp &E, const Slots<K, B> &S, bo
     return __ballot(left) != 0;
 }
 
+// BRX (an in-line side exit): the slots of the group whose condition holds
+// leave for variant E.imm.  Returns whether any slot of the wave is still in
+// the group; `cut` = some slot left it.
+template <int K, int B>
+__device__ __forceinline__ bool apply_brx(const DOp &E, const Slots<K, B> &S, bool (&mine)[K], uint32_t (&sb)[K],
+                                          uint32_t (&steps)[K], bool &cut)
+{
+    const int64_t *a = S.at(E.a);
+    const uint32_t cond = (E.fl >> UF_COND_SHIFT) & 3u;
+    bool left = false, go_any = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t v = sx32(a[k * B], E.fl & UF_TA);
+        const bool take = cond == 0 ? v == 0 : cond == 1 ? v != 0 : cond == 2 ? v > 0 : v < 0;
+        const bool go = mine[k] && take;
+        steps[k] += go ? E.inc : 0u;
+        sb[k] = go ? (uint32_t)E.imm : sb[k];
+        mine[k] = mine[k] && !go;
+        left = left || mine[k];
+        go_any = go_any || go;
+    }
+    cut = __ballot(go_any) != 0;
+    return __ballot(left) != 0;
+}
+
 // Budget-checked variant (taken only by groups that could reach the budget
-// inside a superblock): ROUND_END and OVF may stop single slots.
+// inside a superblock): ROUND_END and OVF may stop single slots, BRX move
+// them to another variant.
 template <int K, int B>
 __device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__restrict__ jtab, uint32_t pc,
                             const SParams &p, const Slots<K, B> &S, uint64_t vlane0, bool (&mine)[K],
@@ -627,6 +653,12 @@ __device__ void run_checked(const DOp *__restrict__ code, const uint32_t *__rest
         if (E.op == U_OVF) {
             bool cut;
             if (!apply_ovf<K, B>(E, S, mine, steps, done, st, outv, cut)) return;
+            ++pc;
+            continue;
+        }
+        if (E.op == U_BRX) {
+            bool cut;
+            if (!apply_brx<K, B>(E, S, mine, sb, steps, cut)) return;
             ++pc;
             continue;
         }
@@ -692,6 +724,13 @@ __device__ __forceinline__ bool sched_step(const DOp *__restrict__ code, const u
         if (E.op == U_OVF) {
             bool cut;
             if (!apply_ovf<K, B>(E, S, mine, steps, fin, st, outv, cut)) return true;
+            full = full && !cut;
+            ++pc;
+            continue;
+        }
+        if (E.op == U_BRX) {
+            bool cut;
+            if (!apply_brx<K, B>(E, S, mine, sb, steps, cut)) return true;
             full = full && !cut;
             ++pc;
             continue;

@@ -118,6 +118,18 @@ int mkc_emulate(void *hv, uint32_t budget, uint32_t cap, int soo, const int64_t 
                     pc++;
                     break;
                 }
+                case mk::U_BRX: {
+                    const int64_t v = sx(reg(I.a), ta);
+                    const uint32_t c = (I.fl >> mk::UF_COND_SHIFT) & 3u;
+                    const bool take = c == 0 ? v == 0 : c == 1 ? v != 0 : c == 2 ? v > 0 : v < 0;
+                    if (take) {
+                        steps += I.inc;
+                        sb = (uint32_t)I.imm;
+                        leave = true;
+                    }
+                    pc++;
+                    break;
+                }
                 case mk::U_OVF:
                     if ((uint64_t)reg(I.b) >= ((uint64_t)I.imm >> 32)) {
                         steps += I.inc;

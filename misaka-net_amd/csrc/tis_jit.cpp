@@ -235,6 +235,7 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
             case U_STX: use(I.a); use(I.b); break;
             case U_LDX: use(I.d); use(I.b); break;
             case U_OVF: if (I.fl & UF_OUTREG) use(I.a); use(I.b); break;
+            case U_BRX: use(I.a); ok = reach(v, (uint64_t)I.imm); break;
             case U_JUMP: ok = reach(v, (uint64_t)I.imm); leave = true; break;
             case U_BR:
                 use(I.a);
@@ -424,7 +425,7 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
     std::vector<size_t> lds;
     for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
         const DOp &I = g.D[pc];
-        if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_OVF) return false;
+        if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_OVF || I.op == U_BRX) return false;
         if (I.op == U_LD) lds.push_back(pc);
     }
     if (lds.empty()) return false;
@@ -523,7 +524,7 @@ void emit_rolled(const OpWriter &w, const Graph &g, const std::vector<Run> &runs
         const DOp &I = g.D[pc];
         if (slot_op(I)) {
             w.data(I, expr(pc, advancing(I)).c_str());
-        } else if (I.op == U_ROUND_END || I.op == U_OVF) { // in-line ends: the shape's callback
+        } else if (I.op == U_ROUND_END || I.op == U_OVF || I.op == U_BRX) { // in-line ends / exits: the shape's callback
             round_end(I, ("(uint64_t)(" + expr(pc, I.inc) + ")").c_str(), pc);
         } else {
             w.data(I);
@@ -665,20 +666,33 @@ void emit_budget_exit(Emitter &e, Emitter &tab, const RoundEnds &re, uint32_t v,
     e.line("    }");
 }
 
-// Whether [lo, hi) holds an OVF (a checked variant with one cannot use the
-// budget-exit lookup: a lane may end at the OVF before its round end).
-bool has_ovf(const Graph &g, size_t lo, size_t hi)
+// Whether [lo, hi) holds an OVF or a BRX (a checked variant with one cannot
+// use the budget-exit lookup: a lane may end or leave there before its
+// round end).
+bool has_inline_exit(const Graph &g, size_t lo, size_t hi)
 {
     for (size_t pc = lo; pc < hi; ++pc)
-        if (g.D[pc].op == U_OVF) return true;
+        if (g.D[pc].op == U_OVF || g.D[pc].op == U_BRX) return true;
     return false;
 }
 
-// In-line ends of a body, in program order: OVF (capacity) and, in checked
-// variants that cannot use the lookup, ROUND_END (budget).  `L` prefixes the
-// lane state ("" or "L."), `fin` is the statement that leaves the lane.
-void emit_inline_end(const OpWriter &w, const DOp &I, const char *inc, const char *L, const char *fin)
+// In-line ends of a body, in program order: OVF (capacity), BRX (a side
+// exit to another variant) and, in checked variants that cannot use the
+// lookup, ROUND_END (budget).  `L` prefixes the lane state ("" or "L."),
+// `fin` is the statement that ends the lane, `go` (a printf format of the
+// target variant) the one that continues it elsewhere.
+void emit_inline_end(const OpWriter &w, const DOp &I, const char *inc, const char *L, const char *fin,
+                     const char *go)
 {
+    if (I.op == U_BRX) {
+        w.e.line("    if %s {", w.cond(I).c_str());
+        w.e.line("        %ssteps += %uu;", L, I.inc);
+        char b[96];
+        snprintf(b, sizeof b, go, (uint32_t)I.imm);
+        w.e.line("        %s", b);
+        w.e.line("    }");
+        return;
+    }
     if (I.op == U_OVF) {
         w.e.line("    if %s {", w.ovf_cond(I).c_str());
         w.e.line("        %ssteps += %uu;", L, I.inc);
@@ -712,22 +726,31 @@ uint64_t max_fast_steps(const SchedProgram &p, const Graph &g)
     std::vector<uint32_t> stack{0u};
     // iterative post-order DFS
     std::vector<uint8_t> state(g.entry.size(), 0);
+    // successors of v with the steps retired on the way to each (a BRX leaves
+    // mid-body with its own count)
+    std::vector<uint64_t> sinc;
     auto exits = [&](uint32_t v, std::vector<uint32_t> &succ) -> uint64_t {
         succ.clear();
+        sinc.clear();
         for (size_t pc = g.entry[v];; ++pc) {
             const DOp &I = g.D[pc];
+            const size_t n0 = succ.size();
             switch (I.op) {
-            case U_JUMP: succ.push_back((uint32_t)I.imm); return I.inc;
+            case U_BRX: succ.push_back((uint32_t)I.imm); sinc.push_back(I.inc); continue;
+            case U_JUMP: succ.push_back((uint32_t)I.imm); break;
             case U_BR:
                 succ.push_back((uint32_t)(uint64_t)I.imm);
                 succ.push_back((uint32_t)((uint64_t)I.imm >> 32));
-                return I.inc;
+                break;
             case U_JRO:
                 for (uint64_t t = 0; t <= I.b; ++t) succ.push_back(p.jtab[(size_t)I.imm + t]);
-                return I.inc;
+                break;
             case U_END: return I.inc;
-            default: break;
+            default: continue;
             }
+            while (sinc.size() < succ.size()) sinc.push_back(I.inc);
+            (void)n0;
+            return I.inc;
         }
     };
     std::vector<uint32_t> succ;
@@ -743,9 +766,9 @@ uint64_t max_fast_steps(const SchedProgram &p, const Graph &g)
         stack.pop_back();
         if (state[v] == 2) continue;
         const uint64_t inc = exits(v, succ);
-        int64_t best = 0;
-        for (uint32_t w : succ) best = std::max<int64_t>(best, memo[w]);
-        memo[v] = (int64_t)inc + best;
+        int64_t best = (int64_t)inc; // END (or no successor)
+        for (size_t k = 0; k < succ.size(); ++k) best = std::max<int64_t>(best, (int64_t)sinc[k] + memo[succ[k]]);
+        memo[v] = best;
         state[v] = 2;
     }
     return (uint64_t)memo[0];
@@ -772,6 +795,7 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
             q.pop_front();
             for (size_t pc = g.entry[v];; ++pc) {
                 const DOp &I = g.D[pc];
+                if (I.op == U_BRX) { add((uint32_t)I.imm); continue; }
                 if (I.op == U_JUMP) { add((uint32_t)I.imm); break; }
                 if (I.op == U_BR) { add((uint32_t)(uint64_t)I.imm); add((uint32_t)((uint64_t)I.imm >> 32)); break; }
                 if (I.op == U_JRO) {
@@ -804,7 +828,7 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
         size_t lo, hi;
         body_range(g, v, lo, hi);
         const RoundEnds re = round_ends(g, v, lo, hi);
-        const bool ovf = has_ovf(g, lo, hi);
+        const bool ovf = has_inline_exit(g, lo, hi);
         if (!re.segs.empty() && !ovf) { // checked variant: always ends at a round end (emit_budget_exit)
             e.line("    {");
             e.line("    int32_t mk_o = 0;");
@@ -820,8 +844,9 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
             e.line("    }");
             continue;
         }
-        emit_body(w, g, v, lo, hi,
-                  [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "", "goto done;"); });
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) {
+            emit_inline_end(w, I, inc, "", "goto done;", "goto V%u;");
+        });
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -934,6 +959,9 @@ bool self_loop(const Graph &g, uint32_t v, size_t &guard_pc, size_t &exit_pc)
         case U_MOV: case U_LI: case U_ADD: case U_SUB: case U_ADDI: case U_RSUBI: case U_ST: case U_STI: case U_LD:
         case U_STX: case U_LDX: case U_OVF:
             continue;
+        case U_BRX: // a side exit at the loop head (a dynamic POP's empty check) only
+            if (pc != guard_pc + 1 || (uint32_t)I.imm == v) return false;
+            continue;
         case U_JUMP:
             exit_pc = pc;
             return (uint32_t)I.imm == v;
@@ -1011,6 +1039,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         case U_STX: R(I.a); R(I.b); break;
         case U_LDX: R(I.b); W(I.d); break;
         case U_OVF: R(I.b); if (I.fl & UF_OUTREG) R(I.a); break;
+        case U_BRX: R(I.a); break;
         default: break;
         }
     }
@@ -1019,8 +1048,12 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     // are discarded by the selects and its steps stop at the iteration's
     // start; the OVF's step count, status and output are recorded and applied
     // after the loop.  Trip counts then come from the per-lane counter.
+    // A BRX at the head (a dynamic POP's empty check, before any other op)
+    // leaves likewise: the lane's registers are the iteration's start, its
+    // step count the loop's so far, and it continues at the BRX's target.
     bool ovf = false;
-    for (size_t pc = gpc + 1; pc < xpc; ++pc) ovf = ovf || g.D[pc].op == U_OVF;
+    for (size_t pc = gpc + 1; pc < xpc; ++pc) ovf = ovf || g.D[pc].op == U_OVF || g.D[pc].op == U_BRX;
+    const DOp *brx = g.D[gpc + 1].op == U_BRX ? &g.D[gpc + 1] : nullptr;
     // induction register: written once per iteration, by r += imm (no truncation)
     int ind = -1;
     int64_t step = 0;
@@ -1059,7 +1092,13 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             const DOp &I = g.D[pc];
             // stores, and indexed loads (a lane that left may hold any index), only for lanes in the loop
             if (I.op == U_ST || I.op == U_STI || I.op == U_STX || I.op == U_LDX) e.line("    if (a)");
-            if (I.op == U_OVF) {
+            if (I.op == U_BRX) {
+                e.line("    {");
+                e.line("    const bool x_ = a && %s;", n.cond(I).c_str());
+                e.line("    brx_ = brx_ || x_;");
+                e.line("    a = a && !x_;");
+                e.line("    }");
+            } else if (I.op == U_OVF) {
                 e.line("    {");
                 e.line("    const bool o_ = a && %s;", n.ovf_cond(I).c_str());
                 e.line("    if (o_) { ovf_ = true; ovs_ = %uu; ovst_ = %uu; ovo_ = %s; }", I.inc, I.d, n.ovf_result(I).c_str());
@@ -1116,9 +1155,10 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
     e.line("    bool a = true, more = true;");
     if (ovf) {
-        e.line("    bool ovf_ = false;");
+        e.line("    bool ovf_ = false, brx_ = false;");
         e.line("    uint32_t ovs_ = 0u, ovst_ = 0u;");
         e.line("    int32_t ovo_ = 0;");
+        e.line("    (void)brx_; (void)ovs_; (void)ovst_; (void)ovo_;");
     }
     e.line("    {");
     e.line("    const uint32_t s0 = L.steps;");
@@ -1172,6 +1212,13 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("    }");
     // a: still in the loop (suspended); otherwise it left through the branch
     // (the condition on its frozen registers fails) or through the guard
+    if (brx) {
+        e.line("    if (brx_) {");
+        e.line("        L.steps += %uu;", brx->inc);
+        e.line("        L.sb = %uu;", (uint32_t)brx->imm);
+        e.line("        break;");
+        e.line("    }");
+    }
     if (ovf) {
         e.line("    if (ovf_) {");
         e.line("        L.steps += ovs_;");
@@ -1291,7 +1338,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         size_t lo, hi;
         body_range(g, v, lo, hi);
         const RoundEnds re = round_ends(g, v, lo, hi);
-        if (!re.segs.empty() && !has_ovf(g, lo, hi)) { // checked variant: always ends at a round end (emit_budget_exit)
+        if (!re.segs.empty() && !has_inline_exit(g, lo, hi)) { // checked variant: always ends at a round end (emit_budget_exit)
             e.line("    int32_t mk_o = 0;");
             emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
                 if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
@@ -1307,9 +1354,10 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             e.line("    }");
             continue;
         }
-        char fin[48];
+        char fin[48], go[48];
         snprintf(fin, sizeof fin, "L.sb = MK_SB_DONE; goto X%u;", v);
-        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "L.", fin); });
+        snprintf(go, sizeof go, "L.sb = %%uu; goto X%u;", v);
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "L.", fin, go); });
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:

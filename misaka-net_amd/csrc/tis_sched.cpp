@@ -382,12 +382,15 @@ class Compiler {
     // Moves every location that is symbolic in any successor into its home
     // register and stores symbolic stack entries.  `keep` is a value the
     // exit op still reads afterwards; returns where to read it.
-    Val canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep);
+    Val canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep,
+                     std::vector<uint8_t> *need_out = nullptr);
+    void rehome(const std::vector<uint8_t> &need);
     void exit_jump();
     void exit_end(uint8_t reason);
     void exit_branch(int n, uint8_t cond, uint16_t target);
     void exit_jro(int n, const Val &v);
     void exit_pop_check(int s);
+    bool inline_pop_check(int s);
     void round_end_marker();
     void generalize();
 
@@ -575,7 +578,8 @@ void Compiler::load_entry(uint32_t id)
     steps_ = 0;
 }
 
-Val Compiler::canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep)
+Val Compiler::canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>> &succ_loc, Val keep,
+                           std::vector<uint8_t> *need_out)
 {
     // 0. dynamic stacks: tracked entries to memory
     for (int s = 0; s < S_; s++) {
@@ -727,6 +731,7 @@ Val Compiler::canonicalize(std::vector<Ctl> &succ, std::vector<std::vector<Val>>
     }
     for (auto &l : lis) emit(U_LI, 0, l.first, 0, 0, l.second);
     if (keep.kind == K_REG) ensure_reg(keep.r);
+    if (need_out) *need_out = need;
     return keep;
 }
 
@@ -791,6 +796,52 @@ void Compiler::exit_jro(int n, const Val &v)
     }
     emit(U_JRO, fa(a), ctl_.ip[n], a.r, (uint16_t)(len - 1), off);
     emit_ext(steps_);
+}
+
+// After a canonicalize() whose trace goes on (an in-line side exit): the
+// values the successors need are in their homes, the others are dead.
+void Compiler::rehome(const std::vector<uint8_t> &need)
+{
+    for (int X = 0; X < L0_; X++) {
+        Val &v = loc_[X];
+        if (v.kind != K_REG && v.kind != K_MEM) continue;
+        if (need[X]) {
+            v = Val();
+            v.kind = K_REG;
+            v.r = (uint16_t)home_[X];
+        } else {
+            v = vdead();
+        }
+    }
+    std::fill(refcnt_.begin(), refcnt_.end(), 0);
+    for (int X = 0; X < L0_; X++) {
+        incref(loc_[X]);
+        if (loc_[X].kind == K_REG) r32_[loc_[X].r] = is32(X);
+    }
+    for (int s = 0; s < S_; s++)
+        for (const Val &e : stk_[s]) incref(e);
+}
+
+// POP from a dynamic stack whose memory part may be empty, in line: the
+// lanes whose DEP is 0 leave through a side exit (BRX) to the state that
+// knows the stack is empty (DEP the constant 0, the same node re-attempts
+// the POP, which blocks); the others go on in this superblock knowing
+// DEP >= 1.  Returns false when the exit could not be made (limits).
+bool Compiler::inline_pop_check(int s)
+{
+    std::vector<Ctl> succ{ctl_};
+    std::vector<std::vector<Val>> sl;
+    std::vector<uint8_t> need;
+    const Val a = canonicalize(succ, sl, loc_[DEP(s)], &need);
+    if (fail_) return false;
+    sl[0][DEP(s)] = vconst(0);
+    const uint32_t it = get_or_create(succ[0], sl[0]);
+    if (fail_) return false;
+    emit(U_BRX, (uint8_t)(fa(a) | (0 << UF_COND_SHIFT)), 0, a.r, 0, 2 * (int64_t)it);
+    emit_ext(steps_);
+    rehome(need);
+    ctl_.lo[s] = 1;
+    return true;
 }
 
 // POP from a dynamic stack whose memory part may be empty: branch on DEP.
@@ -900,12 +951,16 @@ int Compiler::attempt(int n)
             const Val D = loc_[DEP(s)];
             if (D.kind == K_CONST && D.c == 0) return A_CONT;
             if (D.kind == K_REG && ctl_.lo[s] == 0) {
-                exit_pop_check(s);
-                return A_EXIT;
+                if (!lim_.side_exits) {
+                    exit_pop_check(s);
+                    return A_EXIT;
+                }
+                if (!inline_pop_check(s)) return A_EXIT;
             }
+            const Val D2 = loc_[DEP(s)]; // in its home now
             // the memory part holds at least one entry: DEP -= 1, read slot DEP
-            if (D.kind == K_CONST) {
-                set_loc(DEP(s), vconst(D.c - 1));
+            if (D2.kind == K_CONST) {
+                set_loc(DEP(s), vconst(D2.c - 1));
             } else {
                 dep_add(s, -1);
                 ctl_.lo[s]--;
@@ -1151,7 +1206,8 @@ bool Compiler::run(SchedProgram &out, std::string &why)
             if (sc[i].op == U_ROUND_END) {
                 maxinc = std::max<int64_t>(maxinc, sc[i + 1].imm);
                 i++;
-            } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END || sc[i].op == U_OVF) {
+            } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END || sc[i].op == U_OVF ||
+                       sc[i].op == U_BRX) {
                 i++;
             }
         }
@@ -1195,6 +1251,7 @@ SchedLimits lim_env(SchedLimits lim)
     if (const char *e = getenv("MK_SCHED_WIDEN")) lim.widen_after = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_DYN")) lim.dyn_depths = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
+    if (const char *e = getenv("MK_SCHED_SIDE_EXITS")) lim.side_exits = atoi(e) != 0;
     return lim;
 }
 
@@ -1232,7 +1289,8 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
         o.op = u.op;
         o.fl = u.fl;
         o.imm = u.imm;
-        const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF;
+        const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF ||
+                         u.op == U_BRX;
         const uint32_t ext = two ? (uint32_t)p.code[i + 1].imm : 0;
         switch (u.op) {
         case U_MOV: case U_ADDI: case U_RSUBI:
@@ -1247,7 +1305,7 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
             o.d = (uint32_t)u.a | ((uint32_t)u.b << 16); break;
         case U_JUMP: case U_GUARD:
             o.inc = (uint32_t)u.d | ((uint32_t)u.a << 16); break;
-        case U_BR:
+        case U_BR: case U_BRX:
             o.a = u.a * scale; o.inc = ext; break;
         case U_JRO:
             o.d = u.d; o.a = u.a * scale; o.b = u.b; o.inc = ext; break;
@@ -1280,7 +1338,8 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
 std::string sched_disasm(const SchedProgram &p)
 {
     static const char *names[U_COUNT] = {"MOV", "LI",  "ADD", "SUB", "ADDI",  "RSUBI",     "ST",  "STI", "LD",
-                                         "STX", "LDX", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END", "OVF"};
+                                         "STX", "LDX", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END", "OVF",
+                                         "BRX"};
     std::string s;
     char buf[200];
     snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu\n", p.nsb, p.nregs, p.nslots,
@@ -1299,7 +1358,7 @@ std::string sched_disasm(const SchedProgram &p)
         snprintf(buf, sizeof buf, "  %5zu %-9s fl=%02x d=%u a=%u b=%u imm=%lld\n", i, nm, u.fl, u.d, u.a, u.b,
                  (long long)u.imm);
         s += buf;
-        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF) {
+        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF || u.op == U_BRX) {
             i++;
             snprintf(buf, sizeof buf, "        ext       steps+=%lld\n", (long long)p.code[i].imm);
             s += buf;

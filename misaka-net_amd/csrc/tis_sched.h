@@ -39,12 +39,13 @@ enum UOpCode : uint8_t {
     U_ROUND_END,// if steps + ext.imm >= budget: END(status d, out A|imm)          (2 words)
     U_OVF,      // if R[b] >= hi32(ext.imm): steps += lo32(ext.imm); END(status d, out A|imm)
                 // (a PUSH onto a dynamic stack at its capacity)                 (2 words)
+    U_BRX,      // if cond(A): steps += ext.imm; sb = imm (an in-line side exit)  (2 words)
     U_COUNT
 };
 
 constexpr uint8_t U_DATA_LAST = U_LDX; // ops <= this are data micro-ops
 // ops that may stand inside a superblock's body (data ops and in-line ends)
-inline bool body_op(uint32_t op) { return op <= U_DATA_LAST || op == U_ROUND_END || op == U_OVF; }
+inline bool body_op(uint32_t op) { return op <= U_DATA_LAST || op == U_ROUND_END || op == U_OVF || op == U_BRX; }
 
 // A = R[a] (sign-extended low 32 bits when UF_TA), B likewise with UF_TB.
 enum : uint8_t { UF_TA = 1, UF_TB = 2, UF_OUTREG = 4 };
@@ -71,6 +72,7 @@ struct SchedLimits {
     uint64_t max_rounds = 1ull << 22;      // symbolic rounds in total (compile-time bound)
     uint32_t dyn_depths = 24;              // distinct entry depths before a stack turns dynamic (0 = never)
     uint32_t widen_after = 16;             // states of one shape with other constants before widening (0 = never)
+    bool side_exits = true;                // dynamic POP checks as in-line side exits (BRX), else branch exits
 };
 
 struct SchedProgram {
@@ -99,6 +101,7 @@ struct SchedProgram {
 //   STX: a = src offset, b = index offset, imm = base slot   LDX: d, b, imm likewise
 //   OVF: d = status, a = out offset (UF_OUTREG), b = depth offset, inc = steps,
 //        imm = (uint32_t)out value | (uint64_t)limit << 32
+//   BRX: a = cond offset (fl bits 4..5 as BR), imm = target variant, inc = steps
 struct DOp {
     uint32_t op, fl, d, a, b, inc;
     int64_t imm;
