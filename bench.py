@@ -54,6 +54,11 @@ WORKLOADS = {
     "t1_two_stacks": ("t1_two_stacks_1M",
                       lambda: mk.networks.census_classes()["two_stacks_independent_depths"][0][1],
                       1 << 20, N.MK_GEN_MASKED, 255),
+    # the other two census classes: a JRO dispatch loop (8 arms, x >> 3 rounds) and a 16-node ring
+    "t_jro_heavy": ("t_jro_heavy_4M", lambda: mk.networks.census_classes()["jro_heavy"][0][1],
+                    1 << 22, N.MK_GEN_MASKED, 1023),
+    "t_ring16": ("t_ring16_16M", lambda: mk.networks.census_classes()["sixteen_nodes"][0][1],
+                 1 << 24, N.MK_GEN_FULL, 0),
 }
 # Stack-node traffic per lane (PUSH + POP, 4 bytes each), part of the
 # algorithmic bytes: the pipeline's 8 nodes each push `depth` values and pop

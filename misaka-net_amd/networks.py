@@ -152,7 +152,9 @@ def census_classes():
                        "A: JEZ B\nPUSH ACC, s\nSUB 1\nJMP A\n"
                        "B: SWP\nSAV\nC: JEZ D\nPUSH ACC, t\nSUB 1\nJMP C\n"
                        "D: MOV R1, ACC\nOUT ACC"), S("s"), S("t")]
-    # JRO-heavy: a dispatch loop over x & 7 with 8 arms, x >> 3 rounds
+    # JRO-heavy: a loop whose body dispatches through JRO into one of 8 arms;
+    # SAV after ADD 3 reloads the counter each round, so the loop never ends
+    # and every lane runs to the budget (12 node-instructions per round)
     arms = "\n".join(f"ADD {k + 1}\nJMP N" for k in range(8))
     jro_heavy = [P("a", "IN ACC\nSAV\nL: SWP\nJEZ E\nSUB 1\nSWP\nADD 3\nSAV\nJRO 2\n" + arms +
                    "\nN: SWP\nSAV\nSWP\nJMP L\nE: SWP\nOUT ACC")]
