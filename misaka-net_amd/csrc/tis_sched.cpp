@@ -1139,7 +1139,8 @@ void Compiler::compile_entry(uint32_t id)
                 break;
             }
             seen.insert(k);
-            idle = (code_.size() == last_size) ? idle + 1 : 0;
+            // a round that emitted nothing but its own ROUND_END marker (2 words) is idle
+            idle = (code_.size() <= last_size + 2) ? idle + 1 : 0;
             if (idle > lim_.idle_rounds) {
                 generalize();
                 idle = 0;

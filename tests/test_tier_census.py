@@ -25,7 +25,7 @@ def test_random_network_census(capsys):
         for (t, why), n in reasons.most_common(12):
             print(f"  {t:9s} {n:5d}  {why}")
     assert sum(counts.values()) == 1000
-    assert counts["native"] >= 900, counts  # the native tier takes (almost) everything
+    assert counts["native"] >= 995, counts  # the native tier takes (almost) everything
 
 
 @pytest.mark.parametrize("cls", sorted(census_classes()))
