@@ -186,6 +186,44 @@ def valu_peak(stream):
     return ops / (e0.elapsed_time(e1) * 1e-3)
 
 
+def sessions_leg(net, n, calls, stream):
+    """Stateful mode (row f2) at scale: n independent instances of the
+    network, each keeping its node state between calls (program.go:80-92),
+    `calls` sequential /compute calls per instance (mk_session_compute_device
+    per call, inputs and results in HBM), timed with HIP events on `stream`.
+    The session kernel is the interpreter's round structure with the
+    instances' state loaded from and stored back to HBM around each call."""
+    sess = net.sessions(n)
+    sh = stream.cuda_stream
+    x32 = torch.empty(n, dtype=torch.int32, device="cuda")
+    mk.generate_inputs_device(n, x32.data_ptr(), seed=SEED, stream=sh)
+    x = x32.to(torch.int64)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sp = torch.empty(n, dtype=torch.int32, device="cuda")
+    total = torch.zeros((), dtype=torch.int64, device="cuda")
+    outs = torch.zeros((), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    sess.compute_device(x.data_ptr(), out.data_ptr(), st.data_ptr(), sp.data_ptr(), stream=sh)  # warm-up call
+    torch.cuda.synchronize()
+    sess.reset()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(calls):
+        sess.compute_device(x.data_ptr(), out.data_ptr(), st.data_ptr(), sp.data_ptr(), stream=sh)
+        total += sp.to(torch.int64).sum()
+        outs += ((st & 0x10) != 0).sum()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    secs = e0.elapsed_time(e1) * 1e-3
+    sess.close()
+    return {"instances": n, "calls_per_instance": calls, "results_per_s": int(outs) / secs,
+            "node_instr_per_s": int(total) / secs, "ms_per_call": secs / calls * 1e3,
+            "note": "stateful sessions (mk_session_compute_device), inputs resident in HBM; the timed "
+                    "region includes the per-call result reductions; not the value"}
+
+
 def http_leg(nodes, clients, seconds=5.0):
     """Single-value /compute requests through the HTTP master (stateful, the
     reference's semantics; concurrent requests coalesced into one launch per
@@ -249,6 +287,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--sessions", type=int, default=0, metavar="N",
+                    help="also time N stateful instances x 8 sequential /compute calls (row f2; reported as "
+                         "sessions, never as value)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per GPU (default: the config's)")
     ap.add_argument("--gather", action="store_true", help="also time an ordered RCCL gather of outputs to rank 0")
     ap.add_argument("--interp", action="store_true", help="force the tier-1 bytecode interpreter (= --mode interp)")
@@ -528,6 +569,10 @@ def main():
     http = None
     if args.http and rank == 0:
         http = http_leg(nodes, args.http, seconds=5.0)
+    sessions = None
+    if args.sessions and rank == 0:
+        with torch.cuda.stream(stream):  # the per-call reductions on the sessions' stream
+            sessions = sessions_leg(net, args.sessions, 8, stream)
 
     if rank == 0:
         cpu = None
@@ -570,6 +615,8 @@ def main():
             rec["host_io"] = host_io
         if http is not None:
             rec["http"] = http
+        if sessions is not None:
+            rec["sessions"] = sessions
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
