@@ -505,7 +505,10 @@ def main():
     # Lower bound on the launch's memory time: the bytes PMC saw leave the
     # XCDs' L2s at the HBM peak, the algorithmic bytes that never did
     # (stack slots popped back while still in L2) at the L2 peak.
-    fabric = min(traffic, bytes_per_launch) if traffic else bytes_per_launch
+    # Without a matching PMC profile (another lane count), only the streaming
+    # I/O is known to cross HBM: the slot bytes are priced at the L2 peak, a
+    # lower bound on the memory time, so `frac` stays a bound (<= 1).
+    fabric = min(traffic, bytes_per_launch) if traffic else io_bytes
     t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / L2_PEAK
     hbm = {
         "bound": "hbm",
@@ -518,7 +521,9 @@ def main():
         "bytes_per_launch": bytes_per_launch,
         "launch_us": launch_max * 1e6,
         "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
-                  if traffic and bytes_per_launch > fabric * 1.001 else "peak = HBM 8 TB/s"),
+                  if traffic and bytes_per_launch > fabric * 1.001 else
+                  "peak = algorithmic bytes / (I/O bytes / 8 TB/s + stack-slot bytes / 34.5 TB/s): no PMC profile "
+                  "for this launch" if not traffic and slot_bytes else "peak = HBM 8 TB/s"),
         "counter_source": prof.get("source"),
     }
     sq = prof.get("sq", {})
