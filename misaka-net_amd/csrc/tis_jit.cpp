@@ -1657,7 +1657,6 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 // (a wave runs each loop for its longest trip) mostly go away, without the
 // global sort's atomics and scattered result writes (MK_JIT_ORDER).
 static const char *const kMachineSortKernel = R"(
-#define MK_TS_R 4u
 #define MK_TS_T (256u * MK_TS_R)
 #define MK_TS_NB 256u
 // MK_JIT_TS_WAVES asks the allocator for that many waves per SIMD on small
@@ -1688,17 +1687,20 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         const uint64_t base = t * MK_TS_T;
         const uint32_t m = p.n - base < MK_TS_T ? (uint32_t)(p.n - base) : MK_TS_T;
         const bool vec = p.io_vec && m == MK_TS_T;
-        // 1. inputs 4 tid .. 4 tid + 3 of the tile, their range
-        int32_t v[4];
+        // 1. inputs R tid .. R tid + R - 1 of the tile, their range
+        int32_t v[MK_TS_R];
         if (vec) {
-            const int4 q = *reinterpret_cast<const int4 *>((const int32_t *)p.in_data + base + 4u * tid);
-            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            for (uint32_t k = 0; k < MK_TS_R; k += 4u) {
+                const int4 q = *reinterpret_cast<const int4 *>((const int32_t *)p.in_data + base + MK_TS_R * tid + k);
+                v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
+            }
         } else {
-            for (uint32_t k = 0; k < 4u; ++k) v[k] = 4u * tid + k < m ? sched_input(p, base + 4u * tid + k) : 0;
+            for (uint32_t k = 0; k < MK_TS_R; ++k)
+                v[k] = MK_TS_R * tid + k < m ? sched_input(p, base + MK_TS_R * tid + k) : 0;
         }
         uint32_t lo = 0xFFFFFFFFu, hi = 0u; // biased: signed order as unsigned
-        for (uint32_t k = 0; k < 4u; ++k) {
-            if (4u * tid + k >= m) continue;
+        for (uint32_t k = 0; k < MK_TS_R; ++k) {
+            if (MK_TS_R * tid + k >= m) continue;
             const uint32_t b = (uint32_t)v[k] ^ 0x80000000u;
             lo = b < lo ? b : lo;
             hi = b > hi ? b : hi;
@@ -1719,10 +1721,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         const uint32_t span = hi - lo;
         const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
         const uint32_t sh = bits > 8u ? bits - 8u : 0u;
-        uint32_t bk[4];
-        for (uint32_t k = 0; k < 4u; ++k) {
+        uint32_t bk[MK_TS_R];
+        for (uint32_t k = 0; k < MK_TS_R; ++k) {
             bk[k] = (((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh;
-            if (4u * tid + k < m) atomicAdd(&s_cnt[bk[k]], 1u);
+            if (MK_TS_R * tid + k < m) atomicAdd(&s_cnt[bk[k]], 1u);
         }
         __syncthreads();
         // exclusive prefix sum over the 256 buckets (thread tid owns bucket tid)
@@ -1740,11 +1742,11 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             s_cnt[tid] = pre + x - c;
             __syncthreads();
         }
-        for (uint32_t k = 0; k < 4u; ++k) {
-            if (4u * tid + k >= m) continue;
+        for (uint32_t k = 0; k < MK_TS_R; ++k) {
+            if (MK_TS_R * tid + k >= m) continue;
             const uint32_t d = atomicAdd(&s_cnt[bk[k]], 1u);
             s_key[d] = v[k];
-            s_pos[d] = (uint16_t)(4u * tid + k);
+            s_pos[d] = (uint16_t)(MK_TS_R * tid + k);
         }
         __syncthreads();
         // 2. the sorted lanes, 64 per wave and round
@@ -1781,11 +1783,12 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         __syncthreads();
         // 3. results of the tile, in input order
         if (vec) {
-            const uint32_t i = 4u * tid;
-            MK_IO_ST(reinterpret_cast<mk_i32x4 *>(p.out + base + i), (mk_i32x4{s_out[i], s_out[i + 1], s_out[i + 2], s_out[i + 3]}));
-            MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base + i),
-                     (uint32_t)s_st[i] | (uint32_t)s_st[i + 1] << 8 | (uint32_t)s_st[i + 2] << 16 | (uint32_t)s_st[i + 3] << 24);
-            if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base + i) = make_uint4(s_steps[i], s_steps[i + 1], s_steps[i + 2], s_steps[i + 3]);
+            for (uint32_t i = 4u * tid; i < MK_TS_T; i += 1024u) {
+                MK_IO_ST(reinterpret_cast<mk_i32x4 *>(p.out + base + i), (mk_i32x4{s_out[i], s_out[i + 1], s_out[i + 2], s_out[i + 3]}));
+                MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base + i),
+                         (uint32_t)s_st[i] | (uint32_t)s_st[i + 1] << 8 | (uint32_t)s_st[i + 2] << 16 | (uint32_t)s_st[i + 3] << 24);
+                if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base + i) = make_uint4(s_steps[i], s_steps[i + 1], s_steps[i + 2], s_steps[i + 3]);
+            }
         } else {
             for (uint32_t i = tid; i < m; i += 256u) {
                 p.out[base + i] = s_out[i];
@@ -1845,6 +1848,8 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
     num("MK_JIT_TS_WAVES", l.ts_waves);
+    num("MK_JIT_TS_ROUNDS", l.ts_rounds);
+    if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
     return l;
 }
 
@@ -1853,10 +1858,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u",
+             "tsort=%d,tsw=%u,tsr=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves);
+             (int)tile_sort, ts_waves, ts_rounds);
     return b;
 }
 
@@ -2180,6 +2185,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
+    e.line("#define MK_TS_R %uu", lim.ts_rounds);      // kMachineSortKernel: lanes per thread per tile
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks

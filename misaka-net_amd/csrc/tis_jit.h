@@ -91,6 +91,12 @@ struct JitLimits {
     // the register allocator, MK_JIT_TS_WAVES; 0: the compiler's choice --
     // measured best: C5 215 us vs 220 at 8 and 243 at 6, r02l).
     uint32_t ts_waves = 0;
+    // Its tile: 256 x ts_rounds inputs, each wave running ts_rounds sorted
+    // chunks of 64 per tile (MK_JIT_TS_ROUNDS = 4, 8 or 16).  r02v: 8 is 2%
+    // faster on C5 (211 vs 215 us) but 20% / 8% slower on the dynamic-stack
+    // census classes (twice the stack slots in flight per tile); 16 halves
+    // the blocks per CU (61 KB of LDS) and loses everywhere.
+    uint32_t ts_rounds = 4;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
