@@ -1356,6 +1356,7 @@ struct JitState {
     JitShape shape = JIT_STREAM;
     uint64_t max_steps = UINT64_MAX; // stream shape: launches need budget > max_steps
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
+    bool lds = false;                // heavy kernel with the stack slots in LDS (no HBM slots)
     uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
@@ -1785,6 +1786,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     std::string lane;
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
+    J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, lim);
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, lim, J.pool);
@@ -1848,13 +1850,15 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     DeviceGuard g(d);
     const uint64_t block = (uint64_t)sc->jit.block;
     const bool heavy = sc->jit.shape == JIT_STREAM && sc->jit.heavy;
+    // stack slots in HBM (none when the heavy kernel keeps them in LDS)
+    const uint32_t nslots = sc->jit.lds ? 0u : P.nslots;
     // heavy: one thread per input, `chunk` inputs per launch (slot memory);
     // otherwise a resident grid whose threads loop over the inputs
     uint64_t chunk = n, lanes;
     int blocks;
     if (heavy) {
-        if (P.nslots) {
-            const uint64_t fit = h->jit_lim.slot_bytes / ((uint64_t)P.nslots * sizeof(int32_t));
+        if (nslots) {
+            const uint64_t fit = h->jit_lim.slot_bytes / ((uint64_t)nslots * sizeof(int32_t));
             chunk = std::min<uint64_t>(n, std::max<uint64_t>(block, fit / block * block));
         }
         lanes = (std::max<uint64_t>(chunk, 1) + block - 1) / block * block;
@@ -1870,8 +1874,8 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     const uint64_t slot_cols = sc->jit.pool >= 64 ? (uint64_t)blocks * sc->jit.pool
                                : sc->jit.pool      ? lanes * sc->jit.pool
                                                    : lanes;
-    if (P.nslots) {
-        const size_t need = (size_t)P.nslots * slot_cols * sizeof(int32_t);
+    if (nslots) {
+        const size_t need = (size_t)nslots * slot_cols * sizeof(int32_t);
         if (need > sd.slots_bytes) {
             if (sd.d_slots) {
                 (void)hipDeviceSynchronize();
@@ -1899,7 +1903,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     if (counting(d_stats, flags) && (rc = ensure_partials(c, heavy ? 0 : lanes))) return rc;
     p.partials = counting(d_stats, flags) ? c.d_partials : nullptr;
     p.part_rows = (uint32_t)(c.partials_bytes / 64);
-    p.slots = P.nslots ? sd.d_slots : nullptr;
+    p.slots = nslots ? sd.d_slots : nullptr;
     p.lanes = slot_cols;
     p.vlanes = lanes;
     const uintptr_t va = 4u * kJitStreamLanes;
@@ -2730,7 +2734,9 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (t == mk::TIER_NATIVE) {
         char tail[160];
         snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs",
-                 sc->jit.shape == mk::JIT_MACHINE ? "machine" : sc->jit.heavy ? "stream-heavy" : "stream",
+                 sc->jit.shape == mk::JIT_MACHINE ? "machine"
+                 : sc->jit.heavy                  ? (sc->jit.lds ? "stream-heavy-lds" : "stream-heavy")
+                                                  : "stream",
                  sc->jit.pool >= 64 ? ("-pool" + std::to_string(sc->jit.pool)).c_str()
                  : sc->jit.pool     ? ("-k" + std::to_string(sc->jit.pool)).c_str()
                                     : "",

@@ -907,7 +907,24 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
     // MK_JIT_SLOT_LAYOUT=blocked|lane overrides the choice (tests, tuning)
     const bool blocked = g.lim->slot_layout >= 0 ? g.lim->slot_layout == 1 : p.nslots <= kJitWaveBlockedSlots;
     e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
-    if (blocked && g.ndops > g.lim->heavy_ops) {
+    if (jit_slots_in_lds(p.nslots, g.ndops > g.lim->heavy_ops, *g.lim)) {
+        // Heavy kernel, slots in LDS: one wave per block owns nslots x 64
+        // words, slot s of lane l at word s * 64 + l (a wave's access is 64
+        // consecutive words: conflict-free).  No HBM traffic for the stacks.
+        e.line("#ifndef MK_LANE_CHECKED");
+        e.line("#define MK_SLOTS_LDS 1");
+        e.line("__shared__ int32_t mk_lds_slots[MK_NSLOTS * 64u];");
+        e.line("#define MK_SLOT_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
+        e.line("#undef MK_SLOT_ST");
+        e.line("#undef MK_SLOT_LD");
+        e.line("#undef MK_SLOT_STX");
+        e.line("#undef MK_SLOT_LDX");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) (mk_lds_slots[MK_SLOT_IX(s)] = (int32_t)(v))");
+        e.line("#define MK_SLOT_LD(b, ss, s) (mk_lds_slots[MK_SLOT_IX(s)])");
+        e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
+        e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
+        e.line("#endif");
+    } else if (blocked && g.ndops > g.lim->heavy_ops) {
         // Heavy kernel, wave-blocked: `slots` is the wave's block (wave-uniform)
         // and a slot access is a buffer op whose slot offset s * 256 is a
         // scalar (SGPR + immediate) and whose lane offset is one VGPR, so no
@@ -1431,6 +1448,12 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 
 } // namespace
 
+bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
+{
+    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt &&
+           (uint64_t)nslots * 256u <= (uint64_t)lim.lds_slot_bytes;
+}
+
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
                      uint64_t *max_steps, bool *heavy, bool checked, uint32_t *pool)
 {
@@ -1849,6 +1872,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TILE_SORT", l.tile_sort);
     num("MK_JIT_TS_WAVES", l.ts_waves);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
+    num("MK_JIT_LDS_SLOTS", l.lds_slot_bytes);
     if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
     return l;
 }
@@ -1858,10 +1882,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes);
     return b;
 }
 

@@ -28,6 +28,11 @@ constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane p
 // Heavy kernels run one thread per input; a launch covers at most as many
 // inputs as fit this much stack-slot memory (more take several launches).
 constexpr size_t kJitSlotBytes = size_t(16) << 30;
+// Heavy stream kernel: stack slots in LDS up to this many bytes per wave
+// (JitLimits::lds_slot_bytes).  Measured on MI355X (r02x): C4 D=64 (41 shared
+// slots, 10 KB per wave) 194 -> 59 us against its slots in HBM; D=256 (233
+// slots, 58 KB: two waves per CU) 1.14 -> 0.61 ms.
+constexpr size_t kJitLdsSlotBytes = 65536;
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.
 // Measured on MI355X (C5): ahead of every early-refill / early-leave setting
@@ -97,6 +102,11 @@ struct JitLimits {
     // census classes (twice the stack slots in flight per tile); 16 halves
     // the blocks per CU (61 KB of LDS) and loses everywhere.
     uint32_t ts_rounds = 4;
+    // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
+    // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
+    // 0 = never).  One 64-thread block per wave, so the bound also sets the
+    // waves per CU the LDS allows (160 KiB / bytes).
+    size_t lds_slot_bytes = kJitLdsSlotBytes;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
@@ -123,6 +133,10 @@ struct JitLimits {
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why,
                      JitShape *shape = nullptr, uint64_t *max_steps = nullptr, bool *heavy = nullptr,
                      bool checked = false, uint32_t *pool = nullptr);
+
+// Whether the heavy stream kernel keeps the lane's `nslots` stack slots in
+// LDS (the executor then allocates no HBM slots and launches one grid).
+bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim);
 
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of

@@ -369,6 +369,8 @@ class Compiler {
 
     // ---- liveness of ACC / BAK per node instruction ----------------------
     void liveness();
+    // ---- stacks whose memory slots are never in use together share them --
+    void share_slots();
 
     // ---- state management ---------------------------------------------
     void prune(Ctl &c, std::vector<Val> &loc) const;
@@ -1159,6 +1161,123 @@ void Compiler::compile_entry(uint32_t id)
     code_.clear();
 }
 
+// Slot sharing (the memory analogue of register allocation).  An ordinary
+// stack's entry at depth d has one slot for the whole program (slot_of), so
+// the slot count is the sum of every stack's deepest spill -- C4's eight
+// stacks take 8 x 41 slots at D = 64 although node k drains its stack before
+// node k + 1 pushes (stack.go:95-155 moves nothing between the stacks).
+// When the superblock graph is acyclic, every lane runs its superblocks in
+// one topological order and each superblock front to back (a side exit only
+// skips the rest), so the slot accesses of any lane come in increasing
+// global position (topological rank, index).  A stack's slots hold data at
+// most between its first and last slot access in that order; stacks whose
+// windows do not overlap never hold data at the same time on any lane and
+// may share one slot range (interval colouring; slot = range base + depth,
+// affine in the depth, so tis_jit's loop rolling still sees the same runs).
+// Dynamic stacks keep their ranges [k*cap, (k+1)*cap).  MK_SCHED_SHARE=0
+// turns the pass off (SchedLimits::share_slots).
+void Compiler::share_slots()
+{
+    if (!lim_.share_slots || !any_slot_ || max_slot_ < 2) return;
+    const size_t nsb = sb_code_.size();
+    auto two_words = [](uint8_t op) {
+        return op == U_BR || op == U_JRO || op == U_END || op == U_ROUND_END || op == U_OVF || op == U_BRX;
+    };
+    // superblock successors, then a topological order (Kahn); a cycle keeps the slots as they are
+    std::vector<std::vector<uint32_t>> succ(nsb);
+    for (size_t id = 0; id < nsb; id++) {
+        const std::vector<UOp> &sc = sb_code_[id];
+        for (size_t i = 0; i < sc.size(); i++) {
+            const UOp &u = sc[i];
+            if (u.op == U_JUMP || u.op == U_BRX) succ[id].push_back((uint32_t)(u.imm / 2));
+            else if (u.op == U_BR) {
+                succ[id].push_back((uint32_t)((uint64_t)u.imm & 0xFFFFFFFFu) / 2);
+                succ[id].push_back((uint32_t)((uint64_t)u.imm >> 32) / 2);
+            } else if (u.op == U_JRO) {
+                for (uint32_t t = 0; t <= u.b; t++) succ[id].push_back(jtab_[(size_t)u.imm + t] / 2);
+            }
+            if (two_words(u.op)) i++;
+        }
+    }
+    std::vector<uint32_t> indeg(nsb, 0), order;
+    for (auto &v : succ)
+        for (uint32_t t : v) {
+            if (t >= nsb) return;
+            indeg[t]++;
+        }
+    for (uint32_t id = 0; id < nsb; id++)
+        if (!indeg[id]) order.push_back(id);
+    for (size_t k = 0; k < order.size(); k++)
+        for (uint32_t t : succ[order[k]])
+            if (--indeg[t] == 0) order.push_back(t);
+    if (order.size() != nsb) return; // cyclic
+    // static slot -> (stack, depth); each stack's window of slot accesses
+    std::vector<int> st_of(max_slot_, -1);
+    std::vector<uint32_t> d_of(max_slot_, 0);
+    for (int s = 0; s < (int)slot_id_.size(); s++)
+        for (uint32_t d = 0; d < slot_id_[s].size(); d++)
+            if (slot_id_[s][d] >= 0) st_of[slot_id_[s][d]] = s, d_of[slot_id_[s][d]] = d;
+    const uint32_t base0 = ndyn_ * cap_;
+    auto static_slot = [&](const UOp &u, uint32_t &slot) {
+        if (u.op == U_ST || u.op == U_LD) slot = (uint32_t)u.imm;
+        else if (u.op == U_STI) slot = (uint32_t)u.a | ((uint32_t)u.b << 16);
+        else return false;
+        return slot >= base0 && slot - base0 < max_slot_;
+    };
+    std::vector<int64_t> first(S_, -1), last(S_, -1);
+    std::vector<uint32_t> size(S_, 0);
+    int64_t pos = 0;
+    for (uint32_t id : order) {
+        for (size_t i = 0; i < sb_code_[id].size(); i++, pos++) {
+            const UOp &u = sb_code_[id][i];
+            uint32_t slot;
+            if (static_slot(u, slot)) {
+                const int s = st_of[slot - base0];
+                if (s < 0) return;
+                if (first[s] < 0) first[s] = pos;
+                last[s] = pos;
+                size[s] = std::max(size[s], d_of[slot - base0] + 1);
+            }
+            if (two_words(u.op)) i++, pos++;
+        }
+    }
+    // interval colouring in order of first access: a stack joins the first
+    // range whose stacks all finished before it starts
+    std::vector<int> by_first;
+    for (int s = 0; s < S_; s++)
+        if (first[s] >= 0) by_first.push_back(s);
+    std::sort(by_first.begin(), by_first.end(), [&](int a, int b) { return first[a] < first[b]; });
+    std::vector<int64_t> range_end;
+    std::vector<uint32_t> range_size, range_of(S_, 0);
+    for (int s : by_first) {
+        size_t r = 0;
+        while (r < range_end.size() && range_end[r] >= first[s]) r++;
+        if (r == range_end.size()) range_end.push_back(-1), range_size.push_back(0);
+        range_end[r] = last[s];
+        range_size[r] = std::max(range_size[r], size[s]);
+        range_of[s] = (uint32_t)r;
+    }
+    std::vector<uint32_t> range_base(range_size.size(), 0);
+    uint32_t total = 0;
+    for (size_t r = 0; r < range_size.size(); r++) range_base[r] = total, total += range_size[r];
+    if (total >= max_slot_) return; // nothing shared
+    for (auto &sc : sb_code_)
+        for (size_t i = 0; i < sc.size(); i++) {
+            UOp &u = sc[i];
+            uint32_t slot;
+            if (static_slot(u, slot)) {
+                const uint32_t k = slot - base0, ns = base0 + range_base[range_of[st_of[k]]] + d_of[k];
+                if (u.op == U_STI) u.a = (uint16_t)(ns & 0xFFFF), u.b = (uint16_t)(ns >> 16);
+                else u.imm = ns;
+            }
+            if (two_words(u.op)) i++;
+        }
+    for (int s = 0; s < (int)slot_id_.size(); s++)
+        for (uint32_t d = 0; d < slot_id_[s].size(); d++)
+            if (slot_id_[s][d] >= 0) slot_id_[s][d] = (int32_t)(range_base[range_of[s]] + d);
+    max_slot_ = total;
+}
+
 bool Compiler::run(SchedProgram &out, std::string &why)
 {
     if (N_ > 32) { why = "too many program nodes for the compiler"; return false; }
@@ -1196,6 +1315,7 @@ bool Compiler::run(SchedProgram &out, std::string &why)
         why = why_;
         return false;
     }
+    share_slots();
     // assemble: per superblock a fast variant (GUARD + code without budget
     // markers) and a checked variant (with markers)
     out = SchedProgram();
@@ -1253,6 +1373,7 @@ SchedLimits lim_env(SchedLimits lim)
     if (const char *e = getenv("MK_SCHED_DYN")) lim.dyn_depths = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_SIDE_EXITS")) lim.side_exits = atoi(e) != 0;
+    if (const char *e = getenv("MK_SCHED_SHARE")) lim.share_slots = atoi(e) != 0;
     return lim;
 }
 

@@ -206,6 +206,22 @@ def test_machine_shape_pipeline_compiles_in_bound(depth, monkeypatch):
     assert len(src) < (1 << 20) and "mk_jit_exec" in src
 
 
+def test_pipeline_stacks_share_slots(monkeypatch):
+    # node k drains its stack before node k+1 pushes: the eight stacks share
+    # one slot range (tis_sched.cpp share_slots); MK_SCHED_SHARE=0 gives each
+    # its own.  D=64's shared range fits LDS: the heavy kernel keeps it there.
+    for depth, shared, own in ((64, 41, 328), (256, 233, 1864), (1024, 1001, 8008)):
+        assert sc.jit_lane(mk.networks.pipeline_network(depth))[1] == shared
+        monkeypatch.setenv("MK_SCHED_SHARE", "0")
+        assert sc.jit_lane(mk.networks.pipeline_network(depth))[1] == own
+        monkeypatch.delenv("MK_SCHED_SHARE")
+    plan = mk.Network(mk.networks.pipeline_network(64)).plan(mode="jit")
+    assert "slots=41 " in plan and "shape=stream-heavy-lds " in plan, plan
+    monkeypatch.setenv("MK_JIT_LDS_SLOTS", "0")
+    plan = mk.Network(mk.networks.pipeline_network(64)).plan(mode="jit")
+    assert "shape=stream-heavy " in plan, plan
+
+
 def test_compile_bounds_fall_back_with_reason(monkeypatch):
     # over the source bound: tier 2 runs it, mk_net_plan names the bound
     monkeypatch.setenv("MK_JIT_MAX_SRC", "1000")

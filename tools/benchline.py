@@ -5,6 +5,7 @@ import sys
 label = sys.argv[1] if len(sys.argv) > 1 else ""
 for line in sys.stdin:
     r = json.loads(line)
-    print(f"{label[:70]:70s} {r['value']/1e9:9.1f} G/s launch {r['roofline']['launch_us']:8.1f}us "
+    lds = (r.get("roofline_lds") or {}).get("frac")
+    print(f"{label[:70]:70s} {r['value']/1e9:9.1f} G/s launch {r['roofline_hbm']['launch_us']:8.1f}us "
           f"issue {r['roofline_issue']['frac']:.3f} hbm {r['roofline_hbm']['frac']:.3f} "
-          f"{r['config'].get('executor','')[:60]}")
+          f"lds {'-' if lds is None else format(lds, '.3f')} {r['config'].get('executor','')[:60]}")

@@ -11,6 +11,8 @@ are compile / warm-up launches and are skipped):
     (Infinity-Cache hits included), i.e. what left the XCDs' L2s.
   * SQ counters (one pass of 8 SQ + GRBM_GUI_ACTIVE): VALU / SALU wave-
     instructions, VALU lane cycles, waves, vector memory instructions.
+  * LDS counters (a fourth pass): LDS wave-instructions, bank-conflict and
+    LDS-array cycles (bench.py's LDS bound for stacks kept in LDS).
 The bench line's retired node-instructions per launch comes from the same
 runs (node_instr_per_lane x lanes)."""
 import collections
@@ -51,6 +53,7 @@ for cfg in cfgs:
     fetch = per_dispatch(os.path.join(d, "FETCH_SIZE"))
     write = per_dispatch(os.path.join(d, "WRITE_SIZE"))
     sq = per_dispatch(os.path.join(d, "SQ"))
+    lds = per_dispatch(os.path.join(d, "LDS")) if os.path.isdir(os.path.join(d, "LDS")) else {}
     rec = bench_line(os.path.join(d, "SQ.log"))
     workload = rec["config"]["workload"]
     lanes = rec["config"]["lanes_per_gpu"]
@@ -71,6 +74,7 @@ for cfg in cfgs:
         "retired_per_launch": retired,
         "sq": {k: v for k, v in sq.items() if not k.endswith("_dispatches")},
         "sq_dispatches": sq.get("SQ_INSTS_VALU_dispatches"),
+        "lds": {k: v for k, v in lds.items() if not k.endswith("_dispatches")},
     }
     s = out["sq"]
     if s.get("SQ_INSTS_VALU"):
