@@ -38,11 +38,8 @@ SPEC_LANE_OPS = 256 * 4 * 32 * 2.4e9
 K_LANE_OPS = 4  # algorithmic lane-ops per retired node-instruction
 HBM_PEAK = 8.0e12
 L2_PEAK = 34.5e12  # aggregate XCD L2 bandwidth, MI355X_MICROARCH.md section L2
-# LDS (MI355X_MICROARCH.md section LDS): cycles per wave-instruction per CU of
-# the heavy kernel's slot accesses -- ds_read_b32 2 (128 B/clk), ds_write_b32
-# 4 (64 B/clk: the address and data VGPRs move at 2 cycles per dword).
+# LDS (MI355X_MICROARCH.md section LDS): one LDS array per CU, 256 CUs at 2.4 GHz
 LDS_CUS, LDS_CLOCK = 256, 2.4e9
-LDS_READ_CYC, LDS_WRITE_CYC = 2, 4
 
 WORKLOADS = {
     # name: (workload, network factory, lanes per GPU, generator kind, mask)
@@ -581,21 +578,22 @@ def main():
             "peak_measured": None if peak_meas is None else peak_meas / 1e12,
             "launch_us": launch_max * 1e6,
         }
-    # Stack slots in LDS: the slot accesses the PMC pass counted (SQ_INSTS_LDS
-    # wave-instructions, half stores and half loads: every spilled entry is
-    # written once and read back once) at their per-instruction LDS cost.
+    # Stack slots in LDS: the LDS-array cycles the PMC pass counted
+    # (SQ_LDS_IDX_ACTIVE, summed over the CUs; MI355X_MICROARCH.md section
+    # LDS) per CU against the launch's cycles.  LLVM keeps many LDS-resident
+    # slots in registers (a store it can forward to the load), so the count of
+    # LDS instructions, not the stack's pushes and pops, is the measure.
     lds = None
     if lds_slots:
         lsq = prof.get("lds", {})
-        n_lds = lsq.get("SQ_INSTS_LDS")
-        if n_lds:
-            t_lds = n_lds / 2 * (LDS_READ_CYC + LDS_WRITE_CYC) / (LDS_CUS * LDS_CLOCK)
-            lds = {"bound": "lds", "achieved": n_lds * 256 / launch_max / 1e12,
-                   "peak": n_lds * 256 / t_lds / 1e12, "unit": "TB/s", "frac": t_lds / launch_max,
-                   "traffic": traffic, "lds_wave_instr_per_launch": n_lds,
-                   "bank_conflict_cycles": lsq.get("SQ_LDS_BANK_CONFLICT"),
-                   "model": "PMC SQ_INSTS_LDS x 256 B, half ds_write_b32 (4 cycles / wave-instruction / CU) and "
-                            "half ds_read_b32 (2 cycles), 256 CUs at 2.4 GHz (MI355X_MICROARCH.md section LDS)",
+        cyc = lsq.get("SQ_LDS_IDX_ACTIVE")
+        if cyc:
+            per_cu = cyc / LDS_CUS
+            lds = {"bound": "lds", "achieved": per_cu / launch_max / 1e9, "peak": LDS_CLOCK / 1e9,
+                   "unit": "G LDS-array cycles/s per CU", "frac": per_cu / LDS_CLOCK / launch_max,
+                   "traffic": traffic, "lds_wave_instr_per_launch": lsq.get("SQ_INSTS_LDS"),
+                   "lds_array_cycles_per_launch": cyc, "bank_conflict_cycles": lsq.get("SQ_LDS_BANK_CONFLICT"),
+                   "model": "PMC SQ_LDS_IDX_ACTIVE / 256 CUs / 2.4 GHz per launch (LDS array busy)",
                    "launch_us": launch_max * 1e6, "counter_source": prof.get("source")}
         else:
             lds = {"bound": "lds", "frac": None, "model": "no PMC profile of this kernel: LDS work not measured"}
