@@ -1197,6 +1197,19 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             // the whole body is the induction bump: the flag as an int 0/1,
             // no lane masks (mask-writing VALU ops issue at half rate)
             e.line("    int32_t f = 1;");
+            // A countdown by 1 (x > 0, x -= 1): after one iteration a lane
+            // still in the loop has x > 0, so the next x is >= 0 and its flag
+            // is min_u32(x, 1); a lane that left (f = 0) keeps min_u32(x, 0)
+            // = 0.  f = min_u32(x, f) is one VOP2 op where med3 is VOP3
+            // (twice the issue cycles per wave): the first iteration, whose x
+            // may be any value, uses med3 (MK_JIT_FLAG_MIN=0: med3 throughout).
+            const bool fmin = step == -1 && !std::strcmp(flag, "MK_FLAG_GT") && g.lim->flag_min;
+            if (fmin) {
+                e.line("    it = 1u;");
+                e.line("    x = (int32_t)((uint32_t)x - 1u);");
+                e.line("    f = MK_FLAG_GT(x);");
+                e.line("    more = MK_KEEP(f != 0, need);");
+            }
             e.line("    while (more && T32 - it >= %uu) {", uf);
             e.line("    it += %uu;", uf);
             for (int u = 0; u < uf; ++u) {
@@ -1204,7 +1217,10 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                     e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)f);", step < 0 ? '-' : '+');
                 else
                     e.line("    x = MK_MAD24(f, %d, x);", (int)step);
-                e.line("    f = %s(x);", flag);
+                if (fmin)
+                    e.line("    f = MK_FLAG_MIN(x, f);");
+                else
+                    e.line("    f = %s(x);", flag);
             }
             e.line("    more = MK_KEEP(f != 0, need);");
             e.line("    }");
@@ -1873,6 +1889,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_TS_WAVES", l.ts_waves);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
     num("MK_JIT_LDS_SLOTS", l.lds_slot_bytes);
+    flag("MK_JIT_FLAG_MIN", l.flag_min);
     if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
     return l;
 }
@@ -1882,10 +1899,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min);
     return b;
 }
 
@@ -2215,7 +2232,8 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // phase); inline asm so that LLVM does not turn them back into lane masks
     e.line("MK_FN int32_t mk_flag_gt(int32_t x) { int32_t f; __asm__(\"v_med3_i32 %%0, %%1, 0, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
     e.line("MK_FN int32_t mk_flag_lt(int32_t x) { int32_t f; __asm__(\"v_lshrrev_b32 %%0, 31, %%1\" : \"=v\"(f) : \"v\"(x)); return f; }");
-    e.line("MK_FN int32_t mk_flag_nz(int32_t x) { int32_t f; __asm__(\"v_min_u32 %%0, %%1, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
+    e.line("MK_FN int32_t mk_flag_nz(int32_t x) { int32_t f; __asm__(\"v_min_u32 %%0, 1, %%1\" : \"=v\"(f) : \"v\"(x)); return f; }");
+    e.line("MK_FN int32_t mk_flag_min(int32_t x, int32_t g) { int32_t f; __asm__(\"v_min_u32 %%0, %%1, %%2\" : \"=v\"(f) : \"v\"(x), \"v\"(g)); return f; }");
     e.line("MK_FN int32_t mk_mad24(int32_t f, int32_t k, int32_t x)");
     e.line("{");
     e.line("    int32_t r;");
@@ -2225,6 +2243,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_FLAG_GT(x) mk_flag_gt(x)");
     e.line("#define MK_FLAG_LT(x) mk_flag_lt(x)");
     e.line("#define MK_FLAG_NZ(x) mk_flag_nz(x)");
+    e.line("#define MK_FLAG_MIN(x, f) mk_flag_min((x), (f))");
     e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (lim.slot_nt) {

@@ -107,6 +107,10 @@ struct JitLimits {
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
     // waves per CU the LDS allows (160 KiB / bytes).
     size_t lds_slot_bytes = kJitLdsSlotBytes;
+    // Machine-shape countdown loops (x > 0, x -= 1) keep their int flag by
+    // min_u32(x, f), a VOP2 op, after a first iteration by med3 (VOP3)
+    // (MK_JIT_FLAG_MIN=0: med3 in every iteration).
+    bool flag_min = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key

@@ -35,6 +35,7 @@ HEADER = """#include <cstdint>
 #define MK_FLAG_GT(x) ((int32_t)((x) > 0))
 #define MK_FLAG_LT(x) ((int32_t)((x) < 0))
 #define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
+#define MK_FLAG_MIN(x, f) ((int32_t)((uint32_t)(x) < (uint32_t)(f) ? (uint32_t)(x) : (uint32_t)(f)))
 #define MK_MAD24(f, k, x) ((int32_t)((uint32_t)(x) + (uint32_t)(f) * (uint32_t)(k)))
 """
 
