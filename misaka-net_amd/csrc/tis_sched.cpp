@@ -1166,16 +1166,19 @@ void Compiler::compile_entry(uint32_t id)
 // the slot count is the sum of every stack's deepest spill -- C4's eight
 // stacks take 8 x 41 slots at D = 64 although node k drains its stack before
 // node k + 1 pushes (stack.go:95-155 moves nothing between the stacks).
-// When the superblock graph is acyclic, every lane runs its superblocks in
-// one topological order and each superblock front to back (a side exit only
-// skips the rest), so the slot accesses of any lane come in increasing
-// global position (topological rank, index).  A stack's slots hold data at
-// most between its first and last slot access in that order; stacks whose
-// windows do not overlap never hold data at the same time on any lane and
-// may share one slot range (interval colouring; slot = range base + depth,
-// affine in the depth, so tis_jit's loop rolling still sees the same runs).
-// Dynamic stacks keep their ranges [k*cap, (k+1)*cap).  MK_SCHED_SHARE=0
-// turns the pass off (SchedLimits::share_slots).
+// On one lane a stack's slots hold data at most between its first and last
+// slot access; two stacks may share memory when those windows never overlap
+// on any lane.  A lane runs a superblock front to back (a side exit only
+// skips the rest) and its superblocks one after another, so the windows of
+// A and B overlap on a lane's path only if some access to B lies between two
+// accesses to A (or the reverse).  So A and B interfere when an access to B
+// can be reached from an access to A and can reach one (may-analyses over
+// the superblock graph, loops included: accessed before / after a point on
+// some path; a loop that touches A makes A live all through it).  Stacks
+// that do not interfere share a slot range (greedy colouring; slot = range
+// base + depth, affine in the depth, so tis_jit's loop rolling still sees
+// the same runs).  Dynamic stacks keep their ranges [k*cap, (k+1)*cap).
+// MK_SCHED_SHARE=0 turns the pass off (SchedLimits::share_slots).
 void Compiler::share_slots()
 {
     if (!lim_.share_slots || !any_slot_ || max_slot_ < 2) return;
@@ -1183,7 +1186,7 @@ void Compiler::share_slots()
     auto two_words = [](uint8_t op) {
         return op == U_BR || op == U_JRO || op == U_END || op == U_ROUND_END || op == U_OVF || op == U_BRX;
     };
-    // superblock successors, then a topological order (Kahn); a cycle keeps the slots as they are
+    // superblock successors (exits and side exits)
     std::vector<std::vector<uint32_t>> succ(nsb);
     for (size_t id = 0; id < nsb; id++) {
         const std::vector<UOp> &sc = sb_code_[id];
@@ -1199,61 +1202,87 @@ void Compiler::share_slots()
             if (two_words(u.op)) i++;
         }
     }
-    std::vector<uint32_t> indeg(nsb, 0), order;
     for (auto &v : succ)
-        for (uint32_t t : v) {
+        for (uint32_t t : v)
             if (t >= nsb) return;
-            indeg[t]++;
-        }
-    for (uint32_t id = 0; id < nsb; id++)
-        if (!indeg[id]) order.push_back(id);
-    for (size_t k = 0; k < order.size(); k++)
-        for (uint32_t t : succ[order[k]])
-            if (--indeg[t] == 0) order.push_back(t);
-    if (order.size() != nsb) return; // cyclic
-    // static slot -> (stack, depth); each stack's window of slot accesses
+    // static slot -> (stack, depth)
     std::vector<int> st_of(max_slot_, -1);
     std::vector<uint32_t> d_of(max_slot_, 0);
     for (int s = 0; s < (int)slot_id_.size(); s++)
         for (uint32_t d = 0; d < slot_id_[s].size(); d++)
             if (slot_id_[s][d] >= 0) st_of[slot_id_[s][d]] = s, d_of[slot_id_[s][d]] = d;
     const uint32_t base0 = ndyn_ * cap_;
-    auto static_slot = [&](const UOp &u, uint32_t &slot) {
+    auto stack_of = [&](const UOp &u) {
+        uint32_t slot;
         if (u.op == U_ST || u.op == U_LD) slot = (uint32_t)u.imm;
         else if (u.op == U_STI) slot = (uint32_t)u.a | ((uint32_t)u.b << 16);
-        else return false;
-        return slot >= base0 && slot - base0 < max_slot_;
+        else return -1;
+        return slot >= base0 && slot - base0 < max_slot_ ? st_of[slot - base0] : -2;
     };
-    std::vector<int64_t> first(S_, -1), last(S_, -1);
-    std::vector<uint32_t> size(S_, 0);
-    int64_t pos = 0;
-    for (uint32_t id : order) {
-        for (size_t i = 0; i < sb_code_[id].size(); i++, pos++) {
+    // per superblock: first / last access position of each stack; the size of each stack's range
+    const size_t S = (size_t)S_;
+    std::vector<int64_t> first(nsb * S, -1), last(nsb * S, -1);
+    std::vector<uint32_t> size(S, 0);
+    for (size_t id = 0; id < nsb; id++)
+        for (size_t i = 0; i < sb_code_[id].size(); i++) {
             const UOp &u = sb_code_[id][i];
-            uint32_t slot;
-            if (static_slot(u, slot)) {
-                const int s = st_of[slot - base0];
-                if (s < 0) return;
-                if (first[s] < 0) first[s] = pos;
-                last[s] = pos;
+            const int s = stack_of(u);
+            if (s == -2) return; // a slot no stack owns: leave everything alone
+            if (s >= 0) {
+                if (first[id * S + s] < 0) first[id * S + s] = (int64_t)i;
+                last[id * S + s] = (int64_t)i;
+                const uint32_t slot = u.op == U_STI ? ((uint32_t)u.a | ((uint32_t)u.b << 16)) : (uint32_t)u.imm;
                 size[s] = std::max(size[s], d_of[slot - base0] + 1);
             }
-            if (two_words(u.op)) i++, pos++;
+            if (two_words(u.op)) i++;
         }
+    // may-analyses to a fixpoint (loops included): stack accessed on some
+    // path before a superblock's entry / after its exits
+    if ((uint64_t)nsb * S > (uint64_t)1 << 24) return; // bound the analysis
+    std::vector<uint8_t> before(nsb * S, 0), after(nsb * S, 0);
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (size_t id = 0; id < nsb; id++)
+            for (uint32_t t : succ[id])
+                for (size_t s = 0; s < S; s++) {
+                    const uint8_t b = before[id * S + s] | (first[id * S + s] >= 0);
+                    const uint8_t f = after[t * S + s] | (first[t * S + s] >= 0);
+                    if (b && !before[t * S + s]) before[t * S + s] = 1, changed = true;
+                    if (f && !after[id * S + s]) after[id * S + s] = 1, changed = true;
+                }
     }
-    // interval colouring in order of first access: a stack joins the first
-    // range whose stacks all finished before it starts
-    std::vector<int> by_first;
-    for (int s = 0; s < S_; s++)
-        if (first[s] >= 0) by_first.push_back(s);
-    std::sort(by_first.begin(), by_first.end(), [&](int a, int b) { return first[a] < first[b]; });
-    std::vector<int64_t> range_end;
-    std::vector<uint32_t> range_size, range_of(S_, 0);
-    for (int s : by_first) {
+    // A and B interfere when an access to B has A accessed before it and after it
+    std::vector<uint8_t> clash(S * S, 0);
+    for (size_t id = 0; id < nsb; id++)
+        for (size_t i = 0; i < sb_code_[id].size(); i++) {
+            const UOp &u = sb_code_[id][i];
+            const int b = stack_of(u);
+            if (b >= 0)
+                for (size_t a = 0; a < S; a++) {
+                    if ((int)a == b || clash[a * S + b]) continue;
+                    const bool pre = before[id * S + a] || (first[id * S + a] >= 0 && first[id * S + a] < (int64_t)i);
+                    const bool post = after[id * S + a] || last[id * S + a] > (int64_t)i;
+                    if (pre && post) clash[a * S + b] = clash[b * S + a] = 1;
+                }
+            if (two_words(u.op)) i++;
+        }
+    // greedy colouring, largest ranges first: a stack joins the first range
+    // none of whose stacks it interferes with
+    std::vector<int> by_size;
+    for (size_t s = 0; s < S; s++)
+        if (size[s]) by_size.push_back((int)s);
+    std::stable_sort(by_size.begin(), by_size.end(), [&](int a, int b) { return size[a] > size[b]; });
+    std::vector<std::vector<int>> ranges;
+    std::vector<uint32_t> range_size, range_of(S, 0);
+    for (int s : by_size) {
         size_t r = 0;
-        while (r < range_end.size() && range_end[r] >= first[s]) r++;
-        if (r == range_end.size()) range_end.push_back(-1), range_size.push_back(0);
-        range_end[r] = last[s];
+        for (; r < ranges.size(); r++) {
+            bool ok = true;
+            for (int o : ranges[r]) ok = ok && !clash[(size_t)o * S + s];
+            if (ok) break;
+        }
+        if (r == ranges.size()) ranges.emplace_back(), range_size.push_back(0);
+        ranges[r].push_back(s);
         range_size[r] = std::max(range_size[r], size[s]);
         range_of[s] = (uint32_t)r;
     }
@@ -1264,8 +1293,8 @@ void Compiler::share_slots()
     for (auto &sc : sb_code_)
         for (size_t i = 0; i < sc.size(); i++) {
             UOp &u = sc[i];
-            uint32_t slot;
-            if (static_slot(u, slot)) {
+            if (stack_of(u) >= 0) {
+                const uint32_t slot = u.op == U_STI ? ((uint32_t)u.a | ((uint32_t)u.b << 16)) : (uint32_t)u.imm;
                 const uint32_t k = slot - base0, ns = base0 + range_base[range_of[st_of[k]]] + d_of[k];
                 if (u.op == U_STI) u.a = (uint16_t)(ns & 0xFFFF), u.b = (uint16_t)(ns >> 16);
                 else u.imm = ns;

@@ -100,3 +100,43 @@ def test_exit_moves_keep_the_branch_operand():
     a = "IN ACC\nSAV\nL2: NOP\nPUSH ACC, s0\nSWP\nSUB 1\nJGZ L2\nPUSH -1, s0\nMOV R0, ACC\nOUT ACC"
     b = "C: POP s0, ACC\nJLZ E\nSWP\nADD 1\nSWP\nJMP C\nE: SWP\nMOV ACC, a:R0"
     same([("s0", "stack", ""), ("a", "program", a), ("b", "program", b)], np.arange(0, 80))
+
+
+def _push_pop(stk, depth, tag):
+    """PUSH depth values (a+1, a+2, ... for a = ACC) onto `stk`, POP them folding sum = 2*sum + v
+    into ACC."""
+    return ["SAV", f"MOV {depth}, ACC", f"{tag}P: SWP", "ADD 1", f"PUSH ACC, {stk}", "SWP", "SUB 1", f"JGZ {tag}P",
+            "MOV 0, ACC", "SAV", f"MOV {depth}, ACC", f"{tag}Q: SWP", "MOV ACC, a:R3", f"POP {stk}, ACC",
+            "MOV ACC, a:R2", "MOV R3, ACC", "ADD ACC", "ADD R2", "SWP", "SUB 1", f"JGZ {tag}Q", "SWP"]
+
+
+# Stacks share slots only when their windows of slot accesses cannot overlap
+# on any lane (tis_sched.cpp share_slots): used one after the other they
+# share -- also behind a data-dependent branch whose two arms use them in
+# opposite orders, or when only one arm uses one of them -- and interleaved
+# they do not.  Every network is checked against the oracle on the host model.
+@pytest.mark.parametrize("shape", ["sequential", "interleaved", "branch_orders", "branch_one_arm"])
+def test_slot_sharing_is_safe(shape):
+    D = 40
+    S = lambda n: (n, "stack", "")  # noqa: E731
+    if shape == "sequential":
+        body = ["IN ACC"] + _push_pop("s0", D, "A") + _push_pop("s1", D, "B") + ["OUT ACC"]
+    elif shape == "interleaved":
+        push = lambda s, t: [f"MOV {D}, ACC", f"{t}: SWP", "ADD 1", f"PUSH ACC, {s}", "SWP", "SUB 1", f"JGZ {t}"]  # noqa
+        body = (["IN ACC", "SAV"] + push("s0", "P0") + push("s1", "P1") + ["MOV 0, ACC", "SAV"] +
+                [f"MOV {D}, ACC", "L: SWP", "MOV ACC, a:R3", "POP s0, ACC", "MOV ACC, a:R2", "POP s1, ACC",
+                 "ADD R2", "ADD R3", "ADD R3", "ADD R3", "SWP", "SUB 1", "JGZ L", "SWP", "OUT ACC"])
+    elif shape == "branch_orders":
+        body = (["IN ACC", "JGZ POS"] + _push_pop("s0", D, "A") + _push_pop("s1", D, "B") +
+                ["OUT ACC", "JMP E", "POS: NOP"] + _push_pop("s1", D, "C") + _push_pop("s0", D, "F") +
+                ["OUT ACC", "E: NOP"])
+    else:
+        body = (["IN ACC", "JGZ POS"] + _push_pop("s0", D, "A") + ["POS: NOP"] + _push_pop("s1", D, "B") +
+                ["OUT ACC"])
+    nodes = [("a", "program", "\n".join(body)), S("s0"), S("s1")]
+    xs = po.gen_inputs(SEED, 300)
+    xs[:4] = [0, 1, -1, 2147483647]
+    same(nodes, xs)
+    slots = sc.jit_lane(nodes)[1]
+    own = (D - 23) * 2  # each stack's spilled depths, unshared
+    assert (slots < own) == (shape != "interleaved"), (shape, slots)
