@@ -1466,8 +1466,9 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
 {
-    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt &&
-           (uint64_t)nslots * 256u <= (uint64_t)lim.lds_slot_bytes;
+    // one workgroup may hold at most the CU's 160 KiB of LDS
+    const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
+    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt && (uint64_t)nslots * 256u <= cap;
 }
 
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
