@@ -1715,9 +1715,11 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
     __shared__ uint8_t s_st[MK_TS_T];
     __shared__ uint32_t s_cnt[MK_TS_NB];
     __shared__ uint32_t s_red[8];
+    __shared__ uint32_t s_next; // MK_TS_DYN: the tile's next chunk
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
     const uint32_t pol = MK_POLICY;
+    (void)wave;
     // counters, wave-uniform (scalar registers): steps, outputs, lanes, and the four end reasons
     uint64_t c_steps = 0u;
     uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
@@ -1746,6 +1748,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             hi = b > hi ? b : hi;
         }
         s_cnt[tid] = 0u;
+        if (tid == 0u) s_next = 0u;
         lo = MK_WAVE_MIN(lo);
         hi = MK_WAVE_MAX(hi);
         if (lane == 0u) {
@@ -1789,9 +1792,22 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             s_pos[d] = (uint16_t)(MK_TS_R * tid + k);
         }
         __syncthreads();
-        // 2. the sorted lanes, 64 per wave and round
-        for (uint32_t r = 0; r < MK_TS_R; ++r) {
+        // 2. the sorted lanes, 64 per chunk: MK_TS_DYN -- a wave that is
+        // free takes the next chunk, highest values first (their loops run
+        // longest where trips follow the value), so the waves reach the
+        // tile's closing barrier together; else each wave's chunks in snake
+        // order
+        for (uint32_t r = 0;; ++r) {
+#if MK_TS_DYN
+            uint32_t cn = 0u;
+            if (lane == 0u) cn = atomicAdd(&s_next, 1u);
+            cn = (uint32_t)__builtin_amdgcn_readfirstlane((int)cn);
+            if (cn >= 4u * MK_TS_R) break;
+            const uint32_t c = 4u * MK_TS_R - 1u - cn;
+#else
+            if (r >= MK_TS_R) break;
             const uint32_t c = r * 4u + ((r & 1u) ? 3u - wave : wave);
+#endif
             const uint32_t j = c * 64u + lane;
             const bool live = j < m;
             MkLane L;
@@ -1891,6 +1907,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
     num("MK_JIT_LDS_SLOTS", l.lds_slot_bytes);
     flag("MK_JIT_FLAG_MIN", l.flag_min);
+    flag("MK_JIT_TS_DYN", l.ts_dyn);
     if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
     return l;
 }
@@ -1900,10 +1917,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn);
     return b;
 }
 
@@ -2228,6 +2245,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
     e.line("#define MK_TS_R %uu", lim.ts_rounds);      // kMachineSortKernel: lanes per thread per tile
+    e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks

@@ -102,6 +102,10 @@ struct JitLimits {
     // census classes (twice the stack slots in flight per tile); 16 halves
     // the blocks per CU (61 KB of LDS) and loses everywhere.
     uint32_t ts_rounds = 4;
+    // Its chunks: taken by whichever wave of the block is free, highest
+    // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
+    // order.
+    bool ts_dyn = false;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the

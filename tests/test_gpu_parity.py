@@ -696,13 +696,20 @@ def test_machine_input_order_is_transparent(gpu, monkeypatch, kind):
         rows = random_network(seed)
         cases.append((f"seed{seed}", rows, (N.MK_GEN_FULL, 0)))
     # "1": global order by value (MK_JIT_ORDER); "0": the default tile-sorted
-    # kernel; "plain": input order (MK_JIT_TILE_SORT=0)
-    variants = {"1": ("1", "1"), "0": ("0", "1"), "plain": ("0", "0")}
+    # kernel; "dyn" / "snake": the tile-sorted kernel with its chunks taken by
+    # free waves / in snake order (MK_JIT_TS_DYN); "plain": input order
+    # (MK_JIT_TILE_SORT=0)
+    variants = {"1": ("1", "1", None), "0": ("0", "1", None), "dyn": ("0", "1", "1"), "snake": ("0", "1", "0"),
+                "plain": ("0", "0", None)}
     for label, nodes, gen in cases:
         res = {}
-        for order, (o, ts) in variants.items():
+        for order, (o, ts, dyn) in variants.items():
             monkeypatch.setenv("MK_JIT_ORDER", o)
             monkeypatch.setenv("MK_JIT_TILE_SORT", ts)
+            if dyn is None:
+                monkeypatch.delenv("MK_JIT_TS_DYN", raising=False)
+            else:
+                monkeypatch.setenv("MK_JIT_TS_DYN", dyn)
             net = mk.Network(nodes)
             if "shape=machine" not in net.plan():
                 monkeypatch.setenv("MK_JIT_SHAPE", "machine")
@@ -715,8 +722,9 @@ def test_machine_input_order_is_transparent(gpu, monkeypatch, kind):
                 res[order] = _device_run(net, n, in_tensor=xs.to(torch.int32).cuda(), in_kind=N.MK_IN_I32)
             else:
                 res[order] = _device_run(net, n, in_tensor=xs.cuda(), in_kind=N.MK_IN_I64)
-        for a, b, c in zip(res["1"], res["0"], res["plain"]):
-            assert np.array_equal(a, b) and np.array_equal(a, c), label
+        for k in ("0", "dyn", "snake", "plain"):
+            for a, b in zip(res["1"], res[k]):
+                assert np.array_equal(a, b), (label, k)
         ref = oracle(nodes, po.gen_inputs(SEED, n, kind=gen[0], mask=gen[1])[-3000:])
         out, st, sp, _ = res["1"]
         assert np.array_equal(out[-3000:], ref[0]) and np.array_equal(st[-3000:], ref[1]) and \
