@@ -1393,9 +1393,10 @@ bool Compiler::run(SchedProgram &out, std::string &why)
 
 } // namespace
 
-// MK_SCHED_WIDEN / MK_SCHED_DYN / MK_SCHED_MAX_SB override the widening
-// threshold, the dynamic-stack trigger and the superblock limit (experiments
-// and tests; unset = the caller's limits).
+// MK_SCHED_WIDEN / MK_SCHED_DYN / MK_SCHED_MAX_SB / MK_SCHED_SOFT_REGS
+// override the widening threshold, the dynamic-stack trigger, the superblock
+// limit and the registers kept before stack entries spill (experiments and
+// tests; unset = the caller's limits).
 SchedLimits lim_env(SchedLimits lim)
 {
     if (const char *e = getenv("MK_SCHED_WIDEN")) lim.widen_after = (uint32_t)atoi(e);
@@ -1403,6 +1404,10 @@ SchedLimits lim_env(SchedLimits lim)
     if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_SIDE_EXITS")) lim.side_exits = atoi(e) != 0;
     if (const char *e = getenv("MK_SCHED_SHARE")) lim.share_slots = atoi(e) != 0;
+    if (const char *e = getenv("MK_SCHED_SOFT_REGS")) {
+        const int v = atoi(e);
+        if (v >= 4 && (uint32_t)v < lim.max_regs) lim.soft_regs = (uint32_t)v;
+    }
     return lim;
 }
 
