@@ -1552,6 +1552,69 @@ void resolve_opts(const mk_opts *o, uint32_t &budget, uint32_t &cap, uint32_t &f
 // the idle slots of finished lanes).
 bool sched_default_tile(const SchedProgram &) { return true; }
 
+// Waves per CU the heavy kernel's LDS-resident slots allow (capped at 4, one
+// per SIMD); 0 when its slots stay in HBM.
+uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
+{
+    if (!jit_slots_in_lds(P.nslots, true, lim)) return 0;
+    const uint64_t bytes = ((uint64_t)P.nslots * 256u + 511u) / 512u * 512u; // LDS allocation granule
+    return std::min<uint32_t>(4u, (uint32_t)((160u * 1024u) / bytes));
+}
+
+// A network that runs on the heavy stream kernel with its stack slots in
+// LDS is latency-bound when they allow fewer than one wave per SIMD (C4
+// D=256: 233 slots, 58 KB, two waves per CU: 0.61 ms).  Keeping more stack
+// entries in registers (SchedLimits::soft_regs) leaves fewer slots: the
+// smallest register count that reaches the most waves (up to four) wins --
+// C4 D=256 at 50 registers: 207 slots, three waves, 0.38 ms (r02ae; D=64,
+// 15 waves already, is fastest at the default 24).  MK_JIT_TUNE_REGS=0 keeps
+// the default.
+void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
+{
+    const JitLimits &jl = h->jit_lim;
+    if (!jl.tune_regs || jl.disabled || !sc->prog.nslots) return;
+    const uint32_t w0 = lds_waves(sc->prog, jl);
+    if (w0 == 0 || w0 >= 4) return;
+    // waves of the program compiled with r registers, 0 unless the native
+    // tier takes it as a heavy stream lane with LDS slots
+    auto waves = [&](uint32_t r, SchedProgram &P) -> uint32_t {
+        SchedLimits l = lim0;
+        l.soft_regs = r;
+        std::string w, src;
+        JitShape shape = JIT_STREAM;
+        bool heavy = false;
+        if (!compile_schedule(h->net, sc->cap, sc->soo, l, P, w)) return 0;
+        if (!jit_lane_source(P, jl, src, w, &shape, nullptr, &heavy) || shape != JIT_STREAM || !heavy) return 0;
+        return lds_waves(P, jl);
+    };
+    {
+        SchedProgram P;
+        if (waves(lim0.soft_regs, P) != w0) return; // not a heavy stream lane
+    }
+    // coarse scan for the most waves, then the fewest registers that reach them
+    uint32_t best_w = w0, best_r = lim0.soft_regs, prev_r = lim0.soft_regs;
+    for (uint32_t r = lim0.soft_regs + 8u; r + 8u <= lim0.max_regs && best_w < 4u; r += 8u) {
+        SchedProgram P;
+        const uint32_t w = waves(r, P);
+        if (!w) break;
+        if (w > best_w) best_w = w, best_r = r;
+        if (best_r != r) prev_r = r;
+        // about one slot fewer per register: stop when the next step is out of reach
+        const uint32_t next = (160u * 1024u / 512u) / (w + 1u) * 2u;
+        if (w < 4u && P.nslots > next && P.nslots - next > lim0.max_regs - 8u - r) break;
+    }
+    if (best_w == w0) return;
+    uint32_t lo = prev_r + 1u, top = best_r;
+    while (lo < top) {
+        const uint32_t mid = (lo + top) / 2u;
+        SchedProgram P;
+        if (waves(mid, P) >= best_w) top = mid;
+        else lo = mid + 1u;
+    }
+    SchedProgram P;
+    if (waves(top, P) >= best_w) sc->prog = std::move(P);
+}
+
 // Caller holds h->mu.  Compiles the schedule for (cap, soo) once.
 SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
 {
@@ -1562,6 +1625,7 @@ SchedCache *get_sched(mk_net *h, uint32_t cap, bool soo)
     sc->soo = soo;
     SchedLimits lim;
     sc->ok = compile_schedule(h->net, cap, soo, lim, sc->prog, sc->why);
+    if (sc->ok) tune_soft_regs(h, sc.get(), lim);
     sc->tile = sc->ok && sched_default_tile(sc->prog);
     h->sched.push_back(std::move(sc));
     return h->sched.back().get();

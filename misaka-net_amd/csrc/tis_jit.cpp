@@ -1908,6 +1908,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_LDS_SLOTS", l.lds_slot_bytes);
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
+    flag("MK_JIT_TUNE_REGS", l.tune_regs);
     if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
     return l;
 }
@@ -1917,10 +1918,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn, (int)tune_regs);
     return b;
 }
 

@@ -115,6 +115,10 @@ struct JitLimits {
     // min_u32(x, f), a VOP2 op, after a first iteration by med3 (VOP3)
     // (MK_JIT_FLAG_MIN=0: med3 in every iteration).
     bool flag_min = true;
+    // Heavy stream networks whose LDS slots allow fewer than four waves per
+    // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
+    // mk_exec.hip tune_soft_regs).
+    bool tune_regs = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
