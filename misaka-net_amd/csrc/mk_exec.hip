@@ -1557,7 +1557,9 @@ bool sched_default_tile(const SchedProgram &) { return true; }
 uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
 {
     if (!jit_slots_in_lds(P.nslots, true, lim)) return 0;
-    const uint64_t bytes = ((uint64_t)P.nslots * 256u + 511u) / 512u * 512u; // LDS allocation granule
+    // LDS allocation granule: measured, 207 slots (52,992 B) fit three waves per
+    // CU and 212 (54,272 B) do not (r02af), so a 2 KiB granule is assumed
+    const uint64_t bytes = ((uint64_t)P.nslots * 256u + 2047u) / 2048u * 2048u;
     return std::min<uint32_t>(4u, (uint32_t)((160u * 1024u) / bytes));
 }
 
@@ -1567,8 +1569,8 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
 // entries in registers (SchedLimits::soft_regs) leaves fewer slots: the
 // smallest register count that reaches the most waves (up to four) wins --
 // C4 D=256 at 50 registers: 207 slots, three waves, 0.38 ms (r02ae; D=64,
-// 15 waves already, is fastest at the default 24).  MK_JIT_TUNE_REGS=0 keeps
-// the default.
+// 15 waves already, is fastest at the default 24; 212 slots stayed at two
+// waves, 0.56 ms, r02af).  MK_JIT_TUNE_REGS=0 keeps the default.
 void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
@@ -1600,7 +1602,7 @@ void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
         if (w > best_w) best_w = w, best_r = r;
         if (best_r != r) prev_r = r;
         // about one slot fewer per register: stop when the next step is out of reach
-        const uint32_t next = (160u * 1024u / 512u) / (w + 1u) * 2u;
+        const uint32_t next = (160u * 1024u / 2048u) / (w + 1u) * 8u;
         if (w < 4u && P.nslots > next && P.nslots - next > lim0.max_regs - 8u - r) break;
     }
     if (best_w == w0) return;

@@ -226,13 +226,13 @@ def test_pipeline_stacks_share_slots(monkeypatch):
 def test_lds_occupancy_tunes_register_count(monkeypatch):
     # C4 D=256's 233 LDS slots allow two waves per CU; keeping more stack
     # entries in registers (mk_exec.hip tune_soft_regs) reaches three
-    # (<= 212 slots of 256 B in 512-B granules); D=64 (15 waves) keeps 24
+    # (<= 208 slots of 256 B in 2-KiB granules); D=64 (15 waves) keeps 24
     def fields(depth):
         plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode="jit")
         return dict(w.split("=", 1) for w in plan.split() if "=" in w)
 
     f = fields(256)
-    assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 212 and int(f["regs"]) > 24, f
+    assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 208 and int(f["regs"]) > 24, f
     assert fields(64)["regs"] == "24"
     monkeypatch.setenv("MK_JIT_TUNE_REGS", "0")
     f = fields(256)
