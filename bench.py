@@ -563,16 +563,21 @@ def main():
             "counter_source": prof.get("source"),
         }
     else:
+        # No PMC profile of this kernel: the executed work is unknown.  The
+        # frozen k = 4 model is reported beside it,
+        # never as the bound: the compiler retires node-instructions for far
+        # less than 4 lane-ops each (registers, LDS; C4 d256 would read 2.6).
         achieved = K_LANE_OPS * instr_per_launch / launch_max
         issue = {
             "bound": "valu",
-            "achieved": achieved / 1e12,
+            "achieved": None,
             "peak": peak / 1e12,
             "unit": "Tlane-op/s",
-            "frac": achieved / peak,
+            "frac": None,
+            "k_model_frac": achieved / peak,
             "traffic": traffic,
-            "model": "k = 4 lane-ops per retired node-instruction (BASELINE.md section 2; no PMC profile for "
-                     "this launch)",
+            "model": "no PMC profile for this launch: executed VALU work not measured (k_model_frac: k = 4 "
+                     "lane-ops per retired node-instruction, BASELINE.md section 2, not a bound)",
             "k_lane_ops_per_instr": K_LANE_OPS,
             "peak_spec": SPEC_LANE_OPS / 1e12,
             "peak_measured": None if peak_meas is None else peak_meas / 1e12,
