@@ -1236,20 +1236,46 @@ void Compiler::share_slots()
             }
             if (two_words(u.op)) i++;
         }
-    // may-analyses to a fixpoint (loops included): stack accessed on some
-    // path before a superblock's entry / after its exits
-    if ((uint64_t)nsb * S > (uint64_t)1 << 24) return; // bound the analysis
-    std::vector<uint8_t> before(nsb * S, 0), after(nsb * S, 0);
-    for (bool changed = true; changed;) {
-        changed = false;
-        for (size_t id = 0; id < nsb; id++)
-            for (uint32_t t : succ[id])
-                for (size_t s = 0; s < S; s++) {
-                    const uint8_t b = before[id * S + s] | (first[id * S + s] >= 0);
-                    const uint8_t f = after[t * S + s] | (first[t * S + s] >= 0);
-                    if (b && !before[t * S + s]) before[t * S + s] = 1, changed = true;
-                    if (f && !after[id * S + s]) after[id * S + s] = 1, changed = true;
-                }
+    // may-analyses to a fixpoint (loops included): stacks accessed on some
+    // path before a superblock's entry / after its exits, as 64-bit sets,
+    // propagated by worklists (a set only grows, so each superblock is
+    // revisited at most S times)
+    if (S > 64) return;
+    std::vector<uint64_t> acc(nsb, 0), bef(nsb, 0), aft(nsb, 0);
+    for (size_t id = 0; id < nsb; id++)
+        for (size_t s = 0; s < S; s++)
+            if (first[id * S + s] >= 0) acc[id] |= 1ull << s;
+    std::vector<std::vector<uint32_t>> pred(nsb);
+    for (uint32_t id = 0; id < nsb; id++)
+        for (uint32_t t : succ[id]) pred[t].push_back(id);
+    std::vector<uint32_t> work;
+    std::vector<uint8_t> queued(nsb, 1);
+    for (uint32_t id = 0; id < nsb; id++) work.push_back(id);
+    while (!work.empty()) { // forward: bef[t] |= bef[id] | acc[id]
+        const uint32_t id = work.back();
+        work.pop_back();
+        queued[id] = 0;
+        for (uint32_t t : succ[id]) {
+            const uint64_t n = bef[t] | bef[id] | acc[id];
+            if (n != bef[t]) {
+                bef[t] = n;
+                if (!queued[t]) queued[t] = 1, work.push_back(t);
+            }
+        }
+    }
+    std::fill(queued.begin(), queued.end(), 1);
+    for (uint32_t id = 0; id < nsb; id++) work.push_back(id);
+    while (!work.empty()) { // backward: aft[p] |= aft[id] | acc[id]
+        const uint32_t id = work.back();
+        work.pop_back();
+        queued[id] = 0;
+        for (uint32_t q : pred[id]) {
+            const uint64_t n = aft[q] | aft[id] | acc[id];
+            if (n != aft[q]) {
+                aft[q] = n;
+                if (!queued[q]) queued[q] = 1, work.push_back(q);
+            }
+        }
     }
     // A and B interfere when an access to B has A accessed before it and after it
     std::vector<uint8_t> clash(S * S, 0);
@@ -1260,8 +1286,8 @@ void Compiler::share_slots()
             if (b >= 0)
                 for (size_t a = 0; a < S; a++) {
                     if ((int)a == b || clash[a * S + b]) continue;
-                    const bool pre = before[id * S + a] || (first[id * S + a] >= 0 && first[id * S + a] < (int64_t)i);
-                    const bool post = after[id * S + a] || last[id * S + a] > (int64_t)i;
+                    const bool pre = ((bef[id] >> a) & 1u) || (first[id * S + a] >= 0 && first[id * S + a] < (int64_t)i);
+                    const bool post = ((aft[id] >> a) & 1u) || last[id * S + a] > (int64_t)i;
                     if (pre && post) clash[a * S + b] = clash[b * S + a] = 1;
                 }
             if (two_words(u.op)) i++;
