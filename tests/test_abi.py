@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 import misaka_net_amd as mk
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -59,3 +61,45 @@ def test_go_adapter_binds_only_declared_symbols():
     types = {"mk_net", "mk_session", "mk_opts", "mk_node_desc", "mk_remote_req", "mk_trace_entry"}
     assert used - types <= set(declared_functions()), used - types - set(declared_functions())
     assert {"mk_net_load", "mk_compute_batch", "mk_session_create", "mk_session_compute"} <= used
+
+
+def _build_c_client(tmp_path):
+    """integration/c/mk_client.c compiled by gcc against include/mk.h and the
+    in-tree library: a compiled (non-Python) client of the boundary, making
+    the cgo backend's calls."""
+    import subprocess
+
+    lib = os.path.dirname(mk._native.LIB_PATH)
+    exe = str(tmp_path / "mk_client")
+    subprocess.check_call(["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "integration", "c", "mk_client.c"), "-L", lib, "-lmisaka_amd",
+                           f"-Wl,-rpath,{lib}", "-o", exe])
+    return exe
+
+
+def test_c_client_load_errors_and_no_gpu(tmp_path):
+    import subprocess
+
+    exe = _build_c_client(tmp_path)
+    r = subprocess.run([exe, "-p", "MOV 1,ACC", "5"], capture_output=True, text=True)
+    assert r.returncode == 2 and r.stdout == "load -2: node misaka1: line 0, 'MOV 1,ACC' not a valid instruction\n"
+    r = subprocess.run([exe, "-p", "JMP NOWHERE", "5"], capture_output=True, text=True)
+    assert r.returncode == 2 and "line 0, label 'NOWHERE' was not declared" in r.stdout
+    import torch
+
+    if not torch.cuda.is_available():  # no GPU here: the compute call fails loudly (MK_EDEVICE)
+        r = subprocess.run([exe, "5"], capture_output=True, text=True)
+        assert r.returncode == 3 and r.stdout == "compute -4\n"
+
+
+@pytest.mark.gpu
+def test_c_client_compute_on_gpu(gpu, tmp_path):
+    import subprocess
+
+    exe = _build_c_client(tmp_path)
+    vals = ["5", "0", "2147483646", "2147483647", "-2147483648", "4294967301"]
+    r = subprocess.run([exe] + vals, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = [line.split() for line in r.stdout.splitlines()]
+    assert [g[1] for g in got] == ["7", "2", "-2147483648", "-2147483647", "-2147483646", "7"]
+    assert all(g[2] == "0x11" and g[3] == "12" for g in got)
