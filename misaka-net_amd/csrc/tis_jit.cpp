@@ -1289,6 +1289,12 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         uint32_t used = 0;
         for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1u : 0u;
         e.line("#define MK_LANE_REGS %uu", used); // 64-bit lane registers (kMachineSortKernel's occupancy)
+        // kMachineSortKernel's tile (JitLimits::ts_rounds = 0): 8 rounds of
+        // 256 lanes when the lane has no stack slots (C5 211 vs 215 us), 4
+        // with them (the census classes' slots in flight, r02v)
+        e.line("#ifndef MK_TS_R");
+        e.line("#define MK_TS_R %uu", p.nslots ? 4u : 8u);
+        e.line("#endif");
     }
     e.line("struct MkLane {");
     for (uint32_t r = 0; r < p.nregs; ++r)
@@ -1909,7 +1915,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
-    if (l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 4;
+    if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
 
@@ -2245,7 +2251,8 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
-    e.line("#define MK_TS_R %uu", lim.ts_rounds);      // kMachineSortKernel: lanes per thread per tile
+    if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
+        e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
