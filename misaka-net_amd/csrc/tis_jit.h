@@ -100,9 +100,10 @@ struct JitLimits {
     // chunks of 64 per tile (MK_JIT_TS_ROUNDS = 4, 8 or 16).  r02v: 8 is 2%
     // faster on C5 (211 vs 215 us) but 20% / 8% slower on the dynamic-stack
     // census classes (twice the stack slots in flight per tile); 16 halves
-    // the blocks per CU (61 KB of LDS) and loses everywhere.  0 (default):
-    // 8 for lanes without stack slots, 4 with them.
-    uint32_t ts_rounds = 0;
+    // the blocks per CU (61 KB of LDS) and loses everywhere.  0: 8 for
+    // lanes without stack slots, 4 with them -- r02ak: C5 212-214 vs 215 us
+    // but the JRO-heavy census class 58.9 vs 52.1 ms, so not the default.
+    uint32_t ts_rounds = 4;
     // Its chunks: taken by whichever wave of the block is free, highest
     // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
     // order.
