@@ -29,10 +29,12 @@ constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane p
 // inputs as fit this much stack-slot memory (more take several launches).
 constexpr size_t kJitSlotBytes = size_t(16) << 30;
 // Heavy stream kernel: stack slots in LDS up to this many bytes per wave
-// (JitLimits::lds_slot_bytes).  Measured on MI355X (r02x): C4 D=64 (41 shared
-// slots, 10 KB per wave) 194 -> 59 us against its slots in HBM; D=256 (233
-// slots, 58 KB: two waves per CU) 1.14 -> 0.61 ms.
-constexpr size_t kJitLdsSlotBytes = 65536;
+// (JitLimits::lds_slot_bytes): two waves per CU.  Measured on MI355X (r02x,
+// r02an): C4 D=64 (41 shared slots, 10 KB per wave) 194 -> 59 us against its
+// slots in HBM; D=256 (233 slots, 58 KB) 1.14 -> 0.61 ms; D=320 (297 slots,
+// 74 KB) 738 -> 498 us; with one wave per CU HBM wins (D=400: 964 vs 1,098 us,
+// D=500 and 640 likewise).
+constexpr size_t kJitLdsSlotBytes = 81920;
 // Default machine-shape policy word (kMachineKernel): generations -- a wave
 // refills only once all its lanes have ended and loops never leave early.
 // Measured on MI355X (C5): ahead of every early-refill / early-leave setting

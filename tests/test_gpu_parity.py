@@ -147,15 +147,18 @@ def signed_pop_network(depth):
 
 
 # Popped values are sign-extended in every slot layout of the heavy kernel
-# (the wave-blocked one reads slots with unsigned 32-bit buffer loads).
-@pytest.mark.parametrize("layout", ["blocked", "lane"])
+# (the wave-blocked one reads slots with unsigned 32-bit buffer loads; "lds"
+# keeps them in LDS, "blocked" / "lane" in HBM).
+@pytest.mark.parametrize("layout", ["blocked", "lane", "lds"])
 @pytest.mark.parametrize("depth", [64, 300])
 def test_heavy_kernel_pops_sign_extend(gpu, monkeypatch, layout, depth):
-    monkeypatch.setenv("MK_JIT_SLOT_LAYOUT", layout)
+    monkeypatch.setenv("MK_JIT_SLOT_LAYOUT", "lane" if layout == "lane" else "blocked")
+    monkeypatch.setenv("MK_JIT_LDS_SLOTS", "163840" if layout == "lds" else "0")
     monkeypatch.setenv("MK_JIT_HEAVY_OPS", "16")
     nodes = signed_pop_network(depth)
     net = mk.Network(nodes)
-    assert "shape=stream-heavy" in net.plan(), net.plan()
+    want = "shape=stream-heavy-lds " if layout == "lds" else "shape=stream-heavy "
+    assert want in net.plan(), net.plan()
     xs = po.gen_inputs(SEED + 7 * depth, 1000)
     ref = oracle(nodes, xs)
     assert {1, -1} <= set(ref[0].tolist())
