@@ -1570,13 +1570,15 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
 // smallest register count that reaches the most waves (up to four) wins --
 // C4 D=256 at 50 registers: 207 slots, three waves, 0.38 ms (r02ae; D=64,
 // 15 waves already, is fastest at the default 24; 212 slots stayed at two
-// waves, 0.56 ms, r02af).  MK_JIT_TUNE_REGS=0 keeps the default.
+// waves, 0.56 ms, r02af).  Heavy stream networks whose slots stay in HBM
+// take up to 64 registers (fewer slot bytes per lane; see below).
+// MK_JIT_TUNE_REGS=0 keeps the default.
 void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
     if (!jl.tune_regs || jl.disabled || !sc->prog.nslots) return;
     const uint32_t w0 = lds_waves(sc->prog, jl);
-    if (w0 == 0 || w0 >= 4) return;
+    if (w0 >= 4) return;
     // waves of the program compiled with r registers, 0 unless the native
     // tier takes it as a heavy stream lane with LDS slots
     auto waves = [&](uint32_t r, SchedProgram &P) -> uint32_t {
@@ -1590,8 +1592,31 @@ void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
         return lds_waves(P, jl);
     };
     {
-        SchedProgram P;
-        if (waves(lim0.soft_regs, P) != w0) return; // not a heavy stream lane
+        std::string src, why;
+        JitShape shape = JIT_STREAM;
+        bool heavy = false;
+        if (!jit_lane_source(sc->prog, jl, src, why, &shape, nullptr, &heavy) || shape != JIT_STREAM || !heavy)
+            return; // not a heavy stream lane
+    }
+    if (w0 == 0) {
+        // Slots in HBM: fewer slot bytes per lane with more entries in
+        // registers (r02ap, 256K lanes: C4 D=400 950 -> 810 us at 64
+        // registers, D=640 1,684 -> 1,473, D=1024 2,922 -> 2,752): the most
+        // registers up to 64 that the native tier still takes.
+        for (uint32_t r = 64u; r > lim0.soft_regs; r -= 8u) {
+            SchedLimits l = lim0;
+            l.soft_regs = r;
+            SchedProgram P;
+            std::string w, src;
+            JitShape shape = JIT_STREAM;
+            bool heavy = false;
+            if (compile_schedule(h->net, sc->cap, sc->soo, l, P, w) &&
+                jit_lane_source(P, jl, src, w, &shape, nullptr, &heavy) && shape == JIT_STREAM && heavy) {
+                sc->prog = std::move(P);
+                return;
+            }
+        }
+        return;
     }
     // coarse scan for the most waves, then the fewest registers that reach them
     uint32_t best_w = w0, best_r = lim0.soft_regs, prev_r = lim0.soft_regs;

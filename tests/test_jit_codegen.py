@@ -226,7 +226,7 @@ def test_pipeline_stacks_share_slots(monkeypatch):
 def test_lds_occupancy_tunes_register_count(monkeypatch):
     # C4 D=256's 233 LDS slots allow two waves per CU; keeping more stack
     # entries in registers (mk_exec.hip tune_soft_regs) reaches three
-    # (<= 208 slots of 256 B in 2-KiB granules); D=64 (15 waves) keeps 24
+    # (<= 208 slots of 256 B in 2-KiB granules); D=64 (15 waves) keeps 24;
     def fields(depth):
         plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode="jit")
         return dict(w.split("=", 1) for w in plan.split() if "=" in w)
@@ -234,6 +234,9 @@ def test_lds_occupancy_tunes_register_count(monkeypatch):
     f = fields(256)
     assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 208 and int(f["regs"]) > 24, f
     assert fields(64)["regs"] == "24"
+    # slots in HBM (D=1024): up to 64 registers, fewer slot bytes per lane
+    f = fields(1024)
+    assert f["shape"] == "stream-heavy" and f["regs"] == "64" and f["slots"] == "961", f
     monkeypatch.setenv("MK_JIT_TUNE_REGS", "0")
     f = fields(256)
     assert f["slots"] == "233" and f["regs"] == "24", f
