@@ -1356,7 +1356,8 @@ struct JitState {
     JitShape shape = JIT_STREAM;
     uint64_t max_steps = UINT64_MAX; // stream shape: launches need budget > max_steps
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
-    bool lds = false;                // heavy kernel with the stack slots in LDS (no HBM slots)
+    bool lds = false;                // heavy kernel with all its stack slots in LDS (no HBM slots)
+    uint32_t lds_n = 0;              // heavy kernel: slots per lane in LDS (the rest in HBM)
     uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
@@ -1878,6 +1879,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
     J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, lim);
+    J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, lim) : 0u;
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, lim, J.pool);
@@ -1942,7 +1944,7 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     const uint64_t block = (uint64_t)sc->jit.block;
     const bool heavy = sc->jit.shape == JIT_STREAM && sc->jit.heavy;
     // stack slots in HBM (none when the heavy kernel keeps them in LDS)
-    const uint32_t nslots = sc->jit.lds ? 0u : P.nslots;
+    const uint32_t nslots = P.nslots - sc->jit.lds_n;
     // heavy: one thread per input, `chunk` inputs per launch (slot memory);
     // otherwise a resident grid whose threads loop over the inputs
     uint64_t chunk = n, lanes;
@@ -2826,7 +2828,9 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         char tail[160];
         snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs",
                  sc->jit.shape == mk::JIT_MACHINE ? "machine"
-                 : sc->jit.heavy                  ? (sc->jit.lds ? "stream-heavy-lds" : "stream-heavy")
+                 : sc->jit.heavy                  ? (sc->jit.lds ? "stream-heavy-lds"
+                                                     : sc->jit.lds_n ? "stream-heavy-split"
+                                                                     : "stream-heavy")
                                                   : "stream",
                  sc->jit.pool >= 64 ? ("-pool" + std::to_string(sc->jit.pool)).c_str()
                  : sc->jit.pool     ? ("-k" + std::to_string(sc->jit.pool)).c_str()

@@ -907,7 +907,42 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
     // MK_JIT_SLOT_LAYOUT=blocked|lane overrides the choice (tests, tuning)
     const bool blocked = g.lim->slot_layout >= 0 ? g.lim->slot_layout == 1 : p.nslots <= kJitWaveBlockedSlots;
     e.line("#define MK_SLOTS_WAVE_BLOCKED %d", blocked ? 1 : 0);
-    if (jit_slots_in_lds(p.nslots, g.ndops > g.lim->heavy_ops, *g.lim)) {
+    const uint32_t nl = jit_lds_slot_count(p.nslots, g.ndops > g.lim->heavy_ops, *g.lim);
+    if (nl && nl < p.nslots) {
+        // Heavy kernel, slots split: the first nl slots of a lane in LDS (as
+        // below), the rest in the wave's HBM block (buffer ops, as after).
+        // A slot number is wave-uniform for ordinary stacks, so the test is a
+        // scalar branch (per lane for dynamic stacks).
+        e.line("#ifndef MK_LANE_CHECKED");
+        e.line("#define MK_SLOTS_BUFFER 1");
+        e.line("#define MK_SLOTS_LDS_N %uu", nl);
+        e.line("#define MK_HBM_NSLOTS (MK_NSLOTS - MK_SLOTS_LDS_N)");
+        e.line("__shared__ int32_t mk_lds_slots[MK_SLOTS_LDS_N * 64u];");
+        e.line("MK_FN __amdgpu_buffer_rsrc_t mk_slot_rsrc(int32_t *b)");
+        e.line("{");
+        e.line("    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)(256u * MK_HBM_NSLOTS), 0x00020000);");
+        e.line("}");
+        e.line("#define MK_SLOT_LANE ((int32_t)((threadIdx.x & 63u) * 4u))");
+        e.line("MK_FN void mk_slot_st(int32_t *b, uint32_t s, int32_t v)");
+        e.line("{");
+        e.line("    if (s < MK_SLOTS_LDS_N) mk_lds_slots[s * 64u + (threadIdx.x & 63u)] = v;");
+        e.line("    else __builtin_amdgcn_raw_buffer_store_b32(v, mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
+        e.line("}");
+        e.line("MK_FN int32_t mk_slot_ld(int32_t *b, uint32_t s)");
+        e.line("{");
+        e.line("    if (s < MK_SLOTS_LDS_N) return mk_lds_slots[s * 64u + (threadIdx.x & 63u)];");
+        e.line("    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
+        e.line("}");
+        e.line("#undef MK_SLOT_ST");
+        e.line("#undef MK_SLOT_LD");
+        e.line("#undef MK_SLOT_STX");
+        e.line("#undef MK_SLOT_LDX");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) mk_slot_st((b), (uint32_t)(s), (int32_t)(v))");
+        e.line("#define MK_SLOT_LD(b, ss, s) mk_slot_ld((b), (uint32_t)(s))");
+        e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
+        e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
+        e.line("#endif");
+    } else if (nl) {
         // Heavy kernel, slots in LDS: one wave per block owns nslots x 64
         // words, slot s of lane l at word s * 64 + l (a wave's access is 64
         // consecutive words: conflict-free).  No HBM traffic for the stacks.
@@ -1470,6 +1505,17 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 
 } // namespace
 
+uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim)
+{
+    if (jit_slots_in_lds(nslots, heavy, lim)) return nslots;
+    if (!lim.lds_split || !heavy || !nslots || lim.slot_layout == 0 || lim.slot_nt) return 0;
+    if (lim.slot_layout < 0 && nslots > kJitWaveBlockedSlots) return 0; // lane-major layout: no split
+    // as many slots as fit the LDS budget in 2 KiB allocation granules
+    const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
+    const uint32_t n = (uint32_t)(cap / 2048u * 8u);
+    return n < nslots ? n : 0;
+}
+
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
 {
     // one workgroup may hold at most the CU's 160 KiB of LDS
@@ -1593,6 +1639,9 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 // loop); the executor launches one thread per input instead, in chunks
 // bounded by the slot memory they need (kJitSlotBytes).
 static const char *const kStreamKernelHeavy = R"(
+#ifndef MK_HBM_NSLOTS
+#define MK_HBM_NSLOTS MK_NSLOTS // slots per lane in the HBM block (all but the LDS-split ones)
+#endif
 extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
 {
     const uint64_t gid = (uint64_t)blockIdx.x * 64u + threadIdx.x;
@@ -1604,9 +1653,9 @@ extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
         // follow one another: a wave's stacks are one block (tis_jit.h)
 #if MK_SLOTS_BUFFER
         // the wave's block; MK_SLOT_ST/LD add the lane's offset
-        int32_t *slots = p.slots ? p.slots + (uint64_t)blockIdx.x * (64ull * MK_NSLOTS) : (int32_t *)0;
+        int32_t *slots = p.slots ? p.slots + (uint64_t)blockIdx.x * (64ull * MK_HBM_NSLOTS) : (int32_t *)0;
 #else
-        int32_t *slots = p.slots ? p.slots + (gid >> 6) * (64ull * MK_NSLOTS) + (gid & 63u) : (int32_t *)0;
+        int32_t *slots = p.slots ? p.slots + (gid >> 6) * (64ull * MK_HBM_NSLOTS) + (gid & 63u) : (int32_t *)0;
 #endif
         const int32_t o = mk_lane_ng(sched_input(p, gid), p.budget, slots, 64u, &s, &t);
 #else
@@ -1915,6 +1964,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
+    flag("MK_JIT_LDS_SPLIT", l.lds_split);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -1924,10 +1974,11 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d,split=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn, (int)tune_regs);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn, (int)tune_regs,
+             (int)lds_split);
     return b;
 }
 

@@ -123,6 +123,10 @@ struct JitLimits {
     // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
     // mk_exec.hip tune_soft_regs).
     bool tune_regs = true;
+    // Heavy stream networks whose slots do not fit lds_slot_bytes keep the
+    // first lds_slot_bytes / 256 of them in LDS and the rest in HBM
+    // (MK_JIT_LDS_SPLIT=1; experiment).
+    bool lds_split = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
@@ -153,6 +157,9 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
 // Whether the heavy stream kernel keeps the lane's `nslots` stack slots in
 // LDS (the executor then allocates no HBM slots and launches one grid).
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim);
+// Slots of the lane the heavy stream kernel keeps in LDS: all (jit_slots_in_lds),
+// the first ones with JitLimits::lds_split, or none.
+uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim);
 
 // Full hiprtc translation unit: prelude, shared device code
 // (mk_device_common.inc), the lane source and the kernel `mk_jit_exec` of

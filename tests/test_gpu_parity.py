@@ -121,13 +121,17 @@ def test_heavy_kernel_slot_layouts(gpu, monkeypatch, layout, depth):
 # Stack slots in LDS (the heavy kernel's wave owns nslots x 64 words) against
 # HBM: MK_JIT_LDS_SLOTS=0 keeps them in HBM; D=256's 233 shared slots (two
 # waves per CU) are in LDS by default; the pipelined POP loops read LDS.
-@pytest.mark.parametrize("lds,depth", [("default", 64), ("0", 64), ("default", 256), ("0", 256)])
+# "split": the first slots of a lane in LDS, the rest in HBM (MK_JIT_LDS_SPLIT).
+@pytest.mark.parametrize("lds,depth", [("default", 64), ("0", 64), ("default", 256), ("0", 256), ("split", 400),
+                                       ("split", 1024)])
 def test_heavy_kernel_slots_in_lds(gpu, monkeypatch, lds, depth):
-    if lds != "default":
+    if lds == "split":
+        monkeypatch.setenv("MK_JIT_LDS_SPLIT", "1")
+    elif lds != "default":
         monkeypatch.setenv("MK_JIT_LDS_SLOTS", lds)
     nodes = mk.networks.pipeline_network(depth)
     net = mk.Network(nodes)
-    want = "shape=stream-heavy " if lds == "0" else "shape=stream-heavy-lds "
+    want = {"0": "shape=stream-heavy ", "split": "shape=stream-heavy-split "}.get(lds, "shape=stream-heavy-lds ")
     assert want in net.plan(), net.plan()
     xs = po.gen_inputs(SEED + 5 * depth, 4100)
     assert_same(net.compute_batch(xs), oracle(nodes, xs), f"c4 D={depth} lds={lds}")
