@@ -1513,7 +1513,10 @@ uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim)
     // as many slots as fit the LDS budget in 2 KiB allocation granules
     const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
     const uint32_t n = (uint32_t)(cap / 2048u * 8u);
-    return n < nslots ? n : 0;
+    // only when LDS takes most of the slots (r02as, 256K lanes: C4 D=400,
+    // 320 of 337 slots in LDS, 798 -> 574 us; D=640, 320 of 577, 1,472 ->
+    // 1,664 us; D=1024 2,763 -> 3,000 us)
+    return n < nslots && (uint64_t)n * 4u >= (uint64_t)nslots * 3u ? n : 0;
 }
 
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)

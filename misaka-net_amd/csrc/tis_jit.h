@@ -124,9 +124,9 @@ struct JitLimits {
     // mk_exec.hip tune_soft_regs).
     bool tune_regs = true;
     // Heavy stream networks whose slots do not fit lds_slot_bytes keep the
-    // first lds_slot_bytes / 256 of them in LDS and the rest in HBM
-    // (MK_JIT_LDS_SPLIT=1; experiment).
-    bool lds_split = false;
+    // first lds_slot_bytes / 256 of them in LDS and the rest in HBM, when
+    // that is at least three quarters of them (MK_JIT_LDS_SPLIT=0: HBM only).
+    bool lds_split = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
