@@ -1516,7 +1516,7 @@ uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim)
     // only when LDS takes most of the slots (r02as, 256K lanes: C4 D=400,
     // 320 of 337 slots in LDS, 798 -> 574 us; D=640, 320 of 577, 1,472 ->
     // 1,664 us; D=1024 2,763 -> 3,000 us)
-    return n < nslots && (uint64_t)n * 4u >= (uint64_t)nslots * 3u ? n : 0;
+    return n < nslots && (uint64_t)n * 100u >= (uint64_t)nslots * lim.lds_split ? n : 0;
 }
 
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
@@ -1967,7 +1967,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
-    flag("MK_JIT_LDS_SPLIT", l.lds_split);
+    num("MK_JIT_LDS_SPLIT", l.lds_split);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -1977,11 +1977,11 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d,split=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d,split=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn, (int)tune_regs,
-             (int)lds_split);
+             lds_split);
     return b;
 }
 

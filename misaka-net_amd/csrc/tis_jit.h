@@ -125,8 +125,8 @@ struct JitLimits {
     bool tune_regs = true;
     // Heavy stream networks whose slots do not fit lds_slot_bytes keep the
     // first lds_slot_bytes / 256 of them in LDS and the rest in HBM, when
-    // that is at least three quarters of them (MK_JIT_LDS_SPLIT=0: HBM only).
-    bool lds_split = true;
+    // that is at least this percentage of them (MK_JIT_LDS_SPLIT; 0: HBM only).
+    uint32_t lds_split = 75;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
