@@ -40,6 +40,7 @@ HBM_PEAK = 8.0e12
 L2_PEAK = 34.5e12  # aggregate XCD L2 bandwidth, MI355X_MICROARCH.md section L2
 # LDS (MI355X_MICROARCH.md section LDS): one LDS array per CU, 256 CUs at 2.4 GHz
 LDS_CUS, LDS_CLOCK = 256, 2.4e9
+LDS_PEAK = 150e12  # aggregate ds_read_b64/b128 bytes/s, the guide's LDS section
 
 WORKLOADS = {
     # name: (workload, network factory, lanes per GPU, generator kind, mask)
@@ -512,8 +513,11 @@ def main():
     # int32 input read, int32 out + u8 status written, stack slots written and read back
     io_bytes = ((0 if args.gen_inputs else 4) + 4 + 1) * lanes
     slot_bytes = 4 * STACK_OPS_PER_LANE.get(args.config, 0) * lanes
-    # the heavy kernel may keep the slots in LDS: then they are no HBM/L2 bytes
+    # the heavy kernel may keep the slots in LDS: then they are no HBM/L2 bytes;
+    # split between LDS and HBM, the bytes PMC did not see leave L2 are priced
+    # at the LDS peak instead of the L2 one (a lower bound on their time)
     lds_slots = "shape=stream-heavy-lds" in plan
+    lds_split = "shape=stream-heavy-split" in plan
     bytes_per_launch = io_bytes + (0 if lds_slots else slot_bytes)
     hbm_achieved = bytes_per_launch / launch_max
     # Lower bound on the launch's memory time: the bytes PMC saw leave the
@@ -523,7 +527,7 @@ def main():
     # I/O is known to cross HBM: the slot bytes are priced at the L2 peak, a
     # lower bound on the memory time, so `frac` stays a bound (<= 1).
     fabric = min(traffic, bytes_per_launch) if traffic else io_bytes
-    t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / L2_PEAK
+    t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / (LDS_PEAK if lds_split else L2_PEAK)
     hbm = {
         "bound": "hbm",
         "achieved": hbm_achieved / 1e9,
@@ -534,7 +538,9 @@ def main():
         "bytes_per_lane": bytes_per_launch // lanes,
         "bytes_per_launch": bytes_per_launch,
         "launch_us": launch_max * 1e6,
-        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
+        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + LDS-resident bytes / 150 TB/s)"
+                  if traffic and lds_split else
+                  "peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
                   if traffic and bytes_per_launch > fabric * 1.001 else
                   "peak = HBM 8 TB/s; stack slots in LDS (roofline_lds)" if lds_slots else
                   "peak = algorithmic bytes / (I/O bytes / 8 TB/s + stack-slot bytes / 34.5 TB/s): no PMC profile "
@@ -589,7 +595,7 @@ def main():
     # slots in registers (a store it can forward to the load), so the count of
     # LDS instructions, not the stack's pushes and pops, is the measure.
     lds = None
-    if lds_slots:
+    if lds_slots or lds_split:
         lsq = prof.get("lds", {})
         cyc = lsq.get("SQ_LDS_IDX_ACTIVE")
         if cyc:

@@ -1369,6 +1369,8 @@ struct SchedCache {
     bool soo = false;
     bool ok = false;
     bool tile = false; // default lane scheduling (sched_default_tile)
+    bool lds_set = false;   // tune_soft_regs chose the heavy kernel's LDS budget ...
+    size_t lds_bytes = 0;   // ... this many bytes of slots per wave (0: slots in HBM)
     std::string why;
     SchedProgram prog;
     SchedDev dev[kMaxDevices];
@@ -1574,10 +1576,64 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
 // waves, 0.56 ms, r02af).  Heavy stream networks whose slots stay in HBM
 // take up to 64 registers (fewer slot bytes per lane; see below).
 // MK_JIT_TUNE_REGS=0 keeps the default.
-void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
+// Whether the native tier takes P as a heavy stream lane.
+bool heavy_stream(const SchedProgram &P, const JitLimits &jl)
+{
+    std::string src, why;
+    JitShape shape = JIT_STREAM;
+    bool heavy = false;
+    return jit_lane_source(P, jl, src, why, &shape, nullptr, &heavy) && shape == JIT_STREAM && heavy;
+}
+
+// Default policy for heavy stream networks (JitLimits::lds_auto): waves per
+// CU first, then as many slots in LDS as those waves leave room for.
+//   * slots that fit LDS at four waves per CU at the default registers: keep
+//     them there (C4 D=64: 41 slots, 15 waves);
+//   * else take the most registers up to 64 the native tier accepts (fewer
+//     slots; r02ap) and the most waves w in 4, 3, 2 whose LDS share (160,
+//     208, 320 slots in 2 KiB granules) holds all the slots or at least
+//     lds_split percent of them (the rest in HBM); none: slots in HBM.
+// Measured (r02av, 256K-512K lanes): C4 D=256 four waves, 160 of 193 slots
+// in LDS 325 us (three waves, all 208 in LDS: 386); D=320 three waves, 208
+// of 257: 302 us (two waves, all in LDS: 497); D=400 two waves, 320 of 337:
+// 571 us (three waves, 208: 661); D=480 two waves, 320 of 417: 655 us (HBM:
+// 1,048); at 64% or less in LDS HBM alone is as fast or faster (r02au).
+void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
-    if (!jl.tune_regs || jl.disabled || !sc->prog.nslots) return;
+    auto bytes = [](uint32_t n) { return ((uint64_t)n * 256u + 2047u) / 2048u * 2048u; };
+    if (!heavy_stream(sc->prog, jl)) return;
+    if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) return; // the knob's budget holds them
+    SchedProgram best = sc->prog;
+    for (uint32_t r = 64u; r > lim0.soft_regs; r -= 8u) {
+        SchedLimits l = lim0;
+        l.soft_regs = r;
+        SchedProgram P;
+        std::string w;
+        if (compile_schedule(h->net, sc->cap, sc->soo, l, P, w) && heavy_stream(P, jl)) {
+            best = std::move(P);
+            break;
+        }
+    }
+    size_t budget = 0;
+    if (jl.lds_slot_bytes)
+        for (uint32_t w = 4; w >= 2; --w) {
+            const uint64_t cap = std::min<uint64_t>(jl.lds_slot_bytes, (160u * 1024u) / w / 2048u * 2048u);
+            const uint64_t k = cap / 256u; // slots of one wave in LDS
+            if (bytes(best.nslots) <= cap || (jl.lds_split && k * 100u >= (uint64_t)best.nslots * jl.lds_split)) {
+                budget = (size_t)cap;
+                break;
+            }
+        }
+    sc->prog = std::move(best);
+    sc->lds_set = true;
+    sc->lds_bytes = budget;
+}
+
+// MK_JIT_LDS_SLOTS set: registers for the fixed LDS budget (see above).
+void tune_soft_regs_fixed(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
+{
+    const JitLimits &jl = h->jit_lim;
     const uint32_t w0 = lds_waves(sc->prog, jl);
     if (w0 >= 4) return;
     // waves of the program compiled with r registers, 0 unless the native
@@ -1641,6 +1697,17 @@ void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
     }
     SchedProgram P;
     if (waves(top, P) >= best_w) sc->prog = std::move(P);
+}
+
+void tune_soft_regs(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
+{
+    const JitLimits &jl = h->jit_lim;
+    if (!jl.tune_regs || jl.disabled || !sc->prog.nslots) return;
+    if (jl.lds_auto) {
+        tune_lds_auto(h, sc, lim0);
+        return;
+    }
+    tune_soft_regs_fixed(h, sc, lim0);
 }
 
 // Caller holds h->mu.  Compiles the schedule for (cap, soo) once.
@@ -1875,14 +1942,16 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
         return false;
     }
     const auto t0 = std::chrono::steady_clock::now();
+    JitLimits L = lim; // the network's LDS budget, when the loader chose one (tune_lds_auto)
+    if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
     std::string lane;
-    if (!jit_lane_source(sc->prog, lim, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
+    if (!jit_lane_source(sc->prog, L, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
     J.heavy = J.heavy && J.shape == JIT_STREAM;
-    J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, lim);
-    J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, lim) : 0u;
+    J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, L);
+    J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, L) : 0u;
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
-    job->src = jit_module_source(lane, J.shape, J.heavy, lim, J.pool);
+    job->src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
     J.src_bytes = job->src.size();
     std::thread(hiprtc_run, job).detach();
     {
@@ -2881,9 +2950,11 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         mk::JitShape shape;
         bool heavy = false;
         uint32_t pool = 0;
-        if (mk::jit_lane_source(sc->prog, h->jit_lim, lane, why, &shape, nullptr, &heavy, false, &pool))
+        mk::JitLimits L = h->jit_lim; // as jit_compile: the network's LDS budget
+        if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
+        if (mk::jit_lane_source(sc->prog, L, lane, why, &shape, nullptr, &heavy, false, &pool))
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
-                                                                    h->jit_lim, pool));
+                                                                    L, pool));
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

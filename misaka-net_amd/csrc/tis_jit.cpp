@@ -1963,7 +1963,10 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TILE_SORT", l.tile_sort);
     num("MK_JIT_TS_WAVES", l.ts_waves);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
-    num("MK_JIT_LDS_SLOTS", l.lds_slot_bytes);
+    if (const char *v = std::getenv("MK_JIT_LDS_SLOTS"); v && *v) {
+        l.lds_slot_bytes = (size_t)std::strtoull(v, nullptr, 10);
+        l.lds_auto = false;
+    }
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
@@ -1977,10 +1980,11 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu,fmin=%d,tsd=%d,tune=%d,split=%u",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, (int)flag_min, (int)ts_dyn, (int)tune_regs,
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)ts_dyn,
+             (int)tune_regs,
              lds_split);
     return b;
 }

@@ -115,6 +115,9 @@ struct JitLimits {
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
     // waves per CU the LDS allows (160 KiB / bytes).
     size_t lds_slot_bytes = kJitLdsSlotBytes;
+    // The loader picks each heavy network's LDS budget and register count
+    // (mk_exec.hip tune_soft_regs) unless MK_JIT_LDS_SLOTS sets the budget.
+    bool lds_auto = true;
     // Machine-shape countdown loops (x > 0, x -= 1) keep their int flag by
     // min_u32(x, f), a VOP2 op, after a first iteration by med3 (VOP3)
     // (MK_JIT_FLAG_MIN=0: med3 in every iteration).

@@ -119,21 +119,20 @@ def test_heavy_kernel_slot_layouts(gpu, monkeypatch, layout, depth):
 
 
 # Stack slots in LDS (the heavy kernel's wave owns nslots x 64 words) against
-# HBM: MK_JIT_LDS_SLOTS=0 keeps them in HBM; D=256's 233 shared slots (two
-# waves per CU) are in LDS by default; the pipelined POP loops read LDS.
-# "split": the first 320 slots of a lane in LDS, the rest in HBM (by default
-# when that is at least three quarters of them: D=400, 480; MK_JIT_LDS_SPLIT).
-@pytest.mark.parametrize("lds,depth", [("default", 64), ("0", 64), ("default", 256), ("0", 256), ("split", 400),
-                                       ("split", 480)])
-def test_heavy_kernel_slots_in_lds(gpu, monkeypatch, lds, depth):
-    if lds == "split":
-        pass
-    elif lds != "default":
+# HBM, and split between them: by default (tune_lds_auto) D=64 in LDS, D=256
+# and D=400 / 480 split (the first 160 / 320 slots in LDS), D=1024 in HBM;
+# MK_JIT_LDS_SLOTS=0 keeps every slot in HBM, 81920 every slot of D=256 in
+# LDS (three waves per CU).  The pipelined POP loops read LDS.
+@pytest.mark.parametrize("lds,depth,shape", [("auto", 64, "lds"), ("0", 64, "heavy"), ("auto", 256, "split"),
+                                             ("0", 256, "heavy"), ("81920", 256, "lds"), ("auto", 400, "split"),
+                                             ("auto", 480, "split")])
+def test_heavy_kernel_slots_in_lds(gpu, monkeypatch, lds, depth, shape):
+    if lds != "auto":
         monkeypatch.setenv("MK_JIT_LDS_SLOTS", lds)
     nodes = mk.networks.pipeline_network(depth)
     net = mk.Network(nodes)
-    want = {"0": "shape=stream-heavy ", "split": "shape=stream-heavy-split "}.get(lds, "shape=stream-heavy-lds ")
-    assert want in net.plan(), net.plan()
+    want = {"heavy": "shape=stream-heavy ", "split": "shape=stream-heavy-split ", "lds": "shape=stream-heavy-lds "}
+    assert want[shape] in net.plan(), net.plan()
     xs = po.gen_inputs(SEED + 5 * depth, 4100)
     assert_same(net.compute_batch(xs), oracle(nodes, xs), f"c4 D={depth} lds={lds}")
 

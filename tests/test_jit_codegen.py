@@ -224,19 +224,26 @@ def test_pipeline_stacks_share_slots(monkeypatch):
 
 
 def test_lds_occupancy_tunes_register_count(monkeypatch):
-    # C4 D=256's 233 LDS slots allow two waves per CU; keeping more stack
-    # entries in registers (mk_exec.hip tune_soft_regs) reaches three
-    # (<= 208 slots of 256 B in 2-KiB granules); D=64 (15 waves) keeps 24;
+    # The loader's policy for heavy networks (mk_exec.hip tune_lds_auto):
+    # D=64's 41 slots fit LDS at four waves per CU: kept, 24 registers; D=256
+    # takes 64 registers (193 slots) and four waves with 160 slots in LDS,
+    # the rest in HBM; D=1024 (961 slots at 64 registers) stays in HBM
     def fields(depth):
         plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode="jit")
         return dict(w.split("=", 1) for w in plan.split() if "=" in w)
 
+    f = fields(64)
+    assert f["shape"] == "stream-heavy-lds" and f["regs"] == "24" and f["slots"] == "41", f
     f = fields(256)
-    assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 208 and int(f["regs"]) > 24, f
-    assert fields(64)["regs"] == "24"
-    # slots in HBM (D=1024): up to 64 registers, fewer slot bytes per lane
+    assert f["shape"] == "stream-heavy-split" and f["regs"] == "64" and f["slots"] == "193", f
     f = fields(1024)
     assert f["shape"] == "stream-heavy" and f["regs"] == "64" and f["slots"] == "961", f
+    # a fixed LDS budget (MK_JIT_LDS_SLOTS): registers for the most waves
+    # with every slot in LDS -- D=256 reaches three (<= 208 slots of 256 B in
+    # 2-KiB granules)
+    monkeypatch.setenv("MK_JIT_LDS_SLOTS", "81920")
+    f = fields(256)
+    assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 208 and int(f["regs"]) > 24, f
     monkeypatch.setenv("MK_JIT_TUNE_REGS", "0")
     f = fields(256)
     assert f["slots"] == "233" and f["regs"] == "24", f
