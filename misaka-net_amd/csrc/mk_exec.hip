@@ -1970,6 +1970,12 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
         }
         J.code = std::move(job->code);
     }
+    if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded
+        if (FILE *f = std::fopen(d, "wb")) {
+            std::fwrite(J.code.data(), 1, J.code.size(), f);
+            std::fclose(f);
+        }
+    }
     J.compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     J.ok = true;
     return true;
