@@ -895,6 +895,17 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
 // The guarded lane (MK_LANE_CHECKED) is for the CPU tests; the executor
 // gives launches with a smaller budget to tier 2.
 // Stream lanes with more than lim.heavy_ops micro-ops run in the heavy kernel.
+// How the heavy kernel reaches its LDS slots.  Volatile (JitLimits::
+// lds_volatile): every push is an LDS store and every pop an LDS load.
+// Otherwise LLVM may forward a store to the load that pops it and keep the
+// value in registers (nothing else touches the wave's LDS), which for deep
+// stacks turns into long chains of register moves (C4 D=256: 1,686 v_mov,
+// 132 VGPRs).
+void emit_lds_access(Emitter &e, const JitLimits &lim)
+{
+    e.line("#define MK_LDS_SLOTS %s", lim.lds_volatile ? "((volatile int32_t *)mk_lds_slots)" : "mk_lds_slots");
+}
+
 void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps, bool checked)
 {
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, acyclic", g.nreach, g.ndops);
@@ -918,6 +929,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOTS_LDS_N %uu", nl);
         e.line("#define MK_HBM_NSLOTS (MK_NSLOTS - MK_SLOTS_LDS_N)");
         e.line("__shared__ int32_t mk_lds_slots[MK_SLOTS_LDS_N * 64u];");
+        emit_lds_access(e, *g.lim);
         e.line("MK_FN __amdgpu_buffer_rsrc_t mk_slot_rsrc(int32_t *b)");
         e.line("{");
         e.line("    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)(256u * MK_HBM_NSLOTS), 0x00020000);");
@@ -925,12 +937,12 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOT_LANE ((int32_t)((threadIdx.x & 63u) * 4u))");
         e.line("MK_FN void mk_slot_st(int32_t *b, uint32_t s, int32_t v)");
         e.line("{");
-        e.line("    if (s < MK_SLOTS_LDS_N) mk_lds_slots[s * 64u + (threadIdx.x & 63u)] = v;");
+        e.line("    if (s < MK_SLOTS_LDS_N) MK_LDS_SLOTS[s * 64u + (threadIdx.x & 63u)] = v;");
         e.line("    else __builtin_amdgcn_raw_buffer_store_b32(v, mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
         e.line("}");
         e.line("MK_FN int32_t mk_slot_ld(int32_t *b, uint32_t s)");
         e.line("{");
-        e.line("    if (s < MK_SLOTS_LDS_N) return mk_lds_slots[s * 64u + (threadIdx.x & 63u)];");
+        e.line("    if (s < MK_SLOTS_LDS_N) return MK_LDS_SLOTS[s * 64u + (threadIdx.x & 63u)];");
         e.line("    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
         e.line("}");
         e.line("#undef MK_SLOT_ST");
@@ -949,13 +961,14 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#ifndef MK_LANE_CHECKED");
         e.line("#define MK_SLOTS_LDS 1");
         e.line("__shared__ int32_t mk_lds_slots[MK_NSLOTS * 64u];");
+        emit_lds_access(e, *g.lim);
         e.line("#define MK_SLOT_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
         e.line("#undef MK_SLOT_ST");
         e.line("#undef MK_SLOT_LD");
         e.line("#undef MK_SLOT_STX");
         e.line("#undef MK_SLOT_LDX");
-        e.line("#define MK_SLOT_ST(b, ss, s, v) (mk_lds_slots[MK_SLOT_IX(s)] = (int32_t)(v))");
-        e.line("#define MK_SLOT_LD(b, ss, s) (mk_lds_slots[MK_SLOT_IX(s)])");
+        e.line("#define MK_SLOT_ST(b, ss, s, v) (MK_LDS_SLOTS[MK_SLOT_IX(s)] = (int32_t)(v))");
+        e.line("#define MK_SLOT_LD(b, ss, s) (MK_LDS_SLOTS[MK_SLOT_IX(s)])");
         e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
         e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
         e.line("#endif");
@@ -1971,6 +1984,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
+    flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -1980,12 +1994,12 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)ts_dyn,
              (int)tune_regs,
-             lds_split);
+             lds_split, (int)lds_volatile);
     return b;
 }
 

@@ -130,6 +130,9 @@ struct JitLimits {
     // first lds_slot_bytes / 256 of them in LDS and the rest in HBM, when
     // that is at least this percentage of them (MK_JIT_LDS_SPLIT; 0: HBM only).
     uint32_t lds_split = 75;
+    // LDS slot accesses as volatile (MK_JIT_LDS_VOLATILE): LLVM keeps every
+    // push and pop in LDS instead of forwarding stores to loads in registers.
+    bool lds_volatile = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
