@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -1888,32 +1890,83 @@ struct HiprtcJob {
     std::vector<char> code;
 };
 
+// The runtime compiler of this ROCm install.  A process that imported
+// PyTorch first has PyTorch's bundled libhiprtc / libamd_comgr loaded (same
+// sonames, an older LLVM), and the linked hiprtc symbols resolve to them: C4
+// D=256's module came out at 132 VGPRs and 325 us instead of 75 and 195 us.
+// So the compiler is loaded from /opt/rocm in a link-map namespace of its own
+// (dlmopen), where it finds its own comgr; MK_HIPRTC names another library,
+// and the linked symbols are the fallback.
+struct Rtc {
+    decltype(&hiprtcCreateProgram) create = &hiprtcCreateProgram;
+    decltype(&hiprtcCompileProgram) compile = &hiprtcCompileProgram;
+    decltype(&hiprtcGetProgramLogSize) log_size = &hiprtcGetProgramLogSize;
+    decltype(&hiprtcGetProgramLog) log = &hiprtcGetProgramLog;
+    decltype(&hiprtcGetErrorString) error = &hiprtcGetErrorString;
+    decltype(&hiprtcGetCodeSize) code_size = &hiprtcGetCodeSize;
+    decltype(&hiprtcGetCode) code = &hiprtcGetCode;
+    decltype(&hiprtcDestroyProgram) destroy = &hiprtcDestroyProgram;
+    std::string from = "linked";
+};
+
+const Rtc &rtc()
+{
+    static const Rtc r = [] {
+        Rtc x;
+        const char *e = std::getenv("MK_HIPRTC");
+        const std::string path = e && *e ? e : "/opt/rocm/lib/libhiprtc.so.7";
+        if (path == "linked") return x;
+        void *h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h) return x;
+        Rtc y;
+        bool all = true;
+        auto get = [&](auto &fn, const char *name) {
+            void *f = dlsym(h, name);
+            all = all && f;
+            if (f) fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(f);
+        };
+        get(y.create, "hiprtcCreateProgram");
+        get(y.compile, "hiprtcCompileProgram");
+        get(y.log_size, "hiprtcGetProgramLogSize");
+        get(y.log, "hiprtcGetProgramLog");
+        get(y.error, "hiprtcGetErrorString");
+        get(y.code_size, "hiprtcGetCodeSize");
+        get(y.code, "hiprtcGetCode");
+        get(y.destroy, "hiprtcDestroyProgram");
+        if (!all) return x;
+        y.from = path;
+        return y;
+    }();
+    return r;
+}
+
 void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
 {
     bool ok = false;
     std::string why;
     std::vector<char> code;
+    const Rtc &R = rtc();
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (R.create(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         why = "hiprtcCreateProgram failed";
     } else {
         const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-        const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+        const hiprtcResult r = R.compile(prog, 3, opts);
         size_t cs = 0;
         if (r != HIPRTC_SUCCESS) {
             size_t ls = 0;
-            (void)hiprtcGetProgramLogSize(prog, &ls);
+            (void)R.log_size(prog, &ls);
             std::string log(ls, '\0');
-            if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
-            why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
-        } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+            if (ls) (void)R.log(prog, &log[0]);
+            why = std::string("hiprtc: ") + R.error(r) + ": " + log.substr(0, 400);
+        } else if (R.code_size(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
             why = "hiprtc produced no code";
         } else {
             code.resize(cs);
-            (void)hiprtcGetCode(prog, code.data());
+            (void)R.code(prog, code.data());
             ok = true;
         }
-        (void)hiprtcDestroyProgram(&prog);
+        (void)R.destroy(&prog);
     }
     std::lock_guard<std::mutex> lk(j->mu);
     j->ok = ok;
