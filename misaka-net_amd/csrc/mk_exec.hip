@@ -27,6 +27,16 @@
 #include <hip/hiprtc.h>
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <fstream>
+#include <iterator>
+
+extern char **environ;
 
 #include <algorithm>
 #include <array>
@@ -1890,54 +1900,74 @@ struct HiprtcJob {
     std::vector<char> code;
 };
 
-// The runtime compiler of this ROCm install.  A process that imported
-// PyTorch first has PyTorch's bundled libhiprtc / libamd_comgr loaded (same
-// sonames, an older LLVM), and the linked hiprtc symbols resolve to them: C4
-// D=256's module came out at 132 VGPRs and 325 us instead of 75 and 195 us.
-// So the compiler is loaded from /opt/rocm in a link-map namespace of its own
-// (dlmopen), where it finds its own comgr; MK_HIPRTC names another library,
-// and the linked symbols are the fallback.
-struct Rtc {
-    decltype(&hiprtcCreateProgram) create = &hiprtcCreateProgram;
-    decltype(&hiprtcCompileProgram) compile = &hiprtcCompileProgram;
-    decltype(&hiprtcGetProgramLogSize) log_size = &hiprtcGetProgramLogSize;
-    decltype(&hiprtcGetProgramLog) log = &hiprtcGetProgramLog;
-    decltype(&hiprtcGetErrorString) error = &hiprtcGetErrorString;
-    decltype(&hiprtcGetCodeSize) code_size = &hiprtcGetCodeSize;
-    decltype(&hiprtcGetCode) code = &hiprtcGetCode;
-    decltype(&hiprtcDestroyProgram) destroy = &hiprtcDestroyProgram;
-    std::string from = "linked";
-};
-
-const Rtc &rtc()
+// The native tier's compiler.  In a process that imported PyTorch first,
+// PyTorch's bundled libhiprtc / libamd_comgr (the same sonames, an older
+// LLVM) are what the linked hiprtc symbols resolve to, and they generate
+// slower code (C4 D=256: 132 VGPRs and 325 us per launch against 75 and
+// 195 us).  So a module is compiled by mk_rtc (csrc/mk_rtc.cpp, built next to
+// this library) as a child process, which loads this ROCm install's
+// compiler; the in-process hiprtc is the fallback when the helper is missing
+// or MK_HIPRTC=linked.  MK_HIPRTC=<path> names another helper.
+std::string rtc_helper()
 {
-    static const Rtc r = [] {
-        Rtc x;
-        const char *e = std::getenv("MK_HIPRTC");
-        const std::string path = e && *e ? e : "/opt/rocm/lib/libhiprtc.so.7";
-        if (path == "linked") return x;
-        void *h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
-        if (!h) return x;
-        Rtc y;
-        bool all = true;
-        auto get = [&](auto &fn, const char *name) {
-            void *f = dlsym(h, name);
-            all = all && f;
-            if (f) fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(f);
-        };
-        get(y.create, "hiprtcCreateProgram");
-        get(y.compile, "hiprtcCompileProgram");
-        get(y.log_size, "hiprtcGetProgramLogSize");
-        get(y.log, "hiprtcGetProgramLog");
-        get(y.error, "hiprtcGetErrorString");
-        get(y.code_size, "hiprtcGetCodeSize");
-        get(y.code, "hiprtcGetCode");
-        get(y.destroy, "hiprtcDestroyProgram");
-        if (!all) return x;
-        y.from = path;
-        return y;
-    }();
-    return r;
+    const char *e = std::getenv("MK_HIPRTC");
+    if (e && *e) return std::strcmp(e, "linked") ? std::string(e) : std::string();
+    Dl_info info{};
+    if (!dladdr(reinterpret_cast<void *>(&rtc_helper), &info) || !info.dli_fname) return {};
+    std::string dir(info.dli_fname);
+    const size_t slash = dir.rfind('/');
+    dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
+    const std::string path = dir + "/mk_rtc";
+    return access(path.c_str(), X_OK) == 0 ? path : std::string();
+}
+
+// Compile `src` with the helper process.  Returns false (why) when the helper
+// could not run; `ok` tells whether it compiled.
+bool rtc_spawn(const std::string &helper, const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+{
+    const char *td = std::getenv("TMPDIR");
+    std::string base = std::string(td && *td ? td : "/tmp") + "/mk_rtc_XXXXXX";
+    std::vector<char> tmpl(base.begin(), base.end());
+    tmpl.push_back('\0');
+    const int fd = mkstemp(tmpl.data());
+    if (fd < 0) return false;
+    const std::string stem(tmpl.data()), in = stem + ".hip", out = stem + ".co", log = stem + ".log";
+    (void)close(fd);
+    bool ran = false;
+    {
+        std::ofstream f(in, std::ios::binary);
+        f << src;
+    }
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
+    char *argv[] = {const_cast<char *>(helper.c_str()), const_cast<char *>(in.c_str()), const_cast<char *>(out.c_str()),
+                    nullptr};
+    pid_t pid = 0;
+    if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv, environ) == 0) {
+        int st = 0;
+        while (waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+        }
+        ran = WIFEXITED(st) && (WEXITSTATUS(st) == 0 || WEXITSTATUS(st) == 1);
+        ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
+        if (ok) {
+            std::ifstream f(out, std::ios::binary);
+            code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+            ok = !code.empty();
+            if (!ok) why = "mk_rtc wrote no code";
+        } else if (ran) {
+            std::ifstream f(log);
+            std::string l((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+            why = l.substr(0, 480);
+        }
+    }
+    posix_spawn_file_actions_destroy(&fa);
+    (void)unlink(in.c_str());
+    (void)unlink(out.c_str());
+    (void)unlink(log.c_str());
+    (void)unlink(stem.c_str());
+    return ran;
 }
 
 void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
@@ -1945,28 +1975,37 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     bool ok = false;
     std::string why;
     std::vector<char> code;
-    const Rtc &R = rtc();
+    const std::string helper = rtc_helper();
+    if (!helper.empty() && rtc_spawn(helper, j->src, ok, why, code)) {
+        std::lock_guard<std::mutex> lk(j->mu);
+        j->ok = ok;
+        j->why = std::move(why);
+        j->code = std::move(code);
+        j->done = true;
+        j->cv.notify_all();
+        return;
+    }
     hiprtcProgram prog;
-    if (R.create(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (hiprtcCreateProgram(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         why = "hiprtcCreateProgram failed";
     } else {
         const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-        const hiprtcResult r = R.compile(prog, 3, opts);
+        const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
         size_t cs = 0;
         if (r != HIPRTC_SUCCESS) {
             size_t ls = 0;
-            (void)R.log_size(prog, &ls);
+            (void)hiprtcGetProgramLogSize(prog, &ls);
             std::string log(ls, '\0');
-            if (ls) (void)R.log(prog, &log[0]);
-            why = std::string("hiprtc: ") + R.error(r) + ": " + log.substr(0, 400);
-        } else if (R.code_size(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+            if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
+            why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
+        } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
             why = "hiprtc produced no code";
         } else {
             code.resize(cs);
-            (void)R.code(prog, code.data());
+            (void)hiprtcGetCode(prog, code.data());
             ok = true;
         }
-        (void)R.destroy(&prog);
+        (void)hiprtcDestroyProgram(&prog);
     }
     std::lock_guard<std::mutex> lk(j->mu);
     j->ok = ok;
