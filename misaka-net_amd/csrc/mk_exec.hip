@@ -35,6 +35,7 @@
 #include <cerrno>
 #include <fstream>
 #include <iterator>
+#include <string_view>
 
 extern char **environ;
 
@@ -1370,6 +1371,7 @@ struct JitState {
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
     bool lds = false;                // heavy kernel with all its stack slots in LDS (no HBM slots)
     uint32_t lds_n = 0;              // heavy kernel: slots per lane in LDS (the rest in HBM)
+    std::string rtc;                 // compiler of the module: "helper" (mk_rtc) or "inproc"
     uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
@@ -1970,43 +1972,86 @@ bool rtc_spawn(const std::string &helper, const std::string &src, bool &ok, std:
     return ran;
 }
 
+// In-process hiprtc (the linked symbols).
+void rtc_inproc(const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+{
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        why = "hiprtcCreateProgram failed";
+        return;
+    }
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    size_t cs = 0;
+    if (r != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        (void)hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
+        why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
+    } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+        why = "hiprtc produced no code";
+    } else {
+        code.resize(cs);
+        (void)hiprtcGetCode(prog, code.data());
+        ok = true;
+    }
+    (void)hiprtcDestroyProgram(&prog);
+}
+
+// VGPRs of the module's kernel: its code-object metadata (msgpack) holds
+// ".vgpr_count" once, followed by a positive integer.  0 when not found.
+uint32_t code_vgprs(const std::vector<char> &c)
+{
+    static const char key[] = "\xab.vgpr_count";
+    const std::string_view v(c.data(), c.size());
+    const size_t i = v.find(std::string_view(key, sizeof key - 1));
+    if (i == std::string_view::npos || i + sizeof key + 2 >= v.size()) return 0;
+    const auto *q = reinterpret_cast<const unsigned char *>(v.data() + i + sizeof key - 1);
+    if (q[0] < 0x80) return q[0];
+    if (q[0] == 0xcc) return q[1];
+    if (q[0] == 0xcd) return (uint32_t)q[1] << 8 | q[2];
+    return 0;
+}
+
+// Whether the linked hiprtc is another install's than the helper's (PyTorch's
+// bundled one in a process that imported it first).
+bool inproc_rtc_differs()
+{
+    Dl_info info{};
+    if (!dladdr(reinterpret_cast<void *>(&hiprtcCompileProgram), &info) || !info.dli_fname) return false;
+    return std::strncmp(info.dli_fname, "/opt/rocm", 9) != 0;
+}
+
 void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
 {
     bool ok = false;
     std::string why;
     std::vector<char> code;
+    // The helper's module (this ROCm's compiler); where the in-process
+    // compiler is another one, its module too, and the one whose kernel
+    // needs fewer VGPRs is kept -- each compiler wins some networks (C4
+    // D=64: 58 vs 94 VGPRs, 59 vs 72 us, for the in-process one; D=256: 75
+    // vs 132 VGPRs, 191 vs 319 us, for the helper's).
     const std::string helper = rtc_helper();
-    if (!helper.empty() && rtc_spawn(helper, j->src, ok, why, code)) {
-        std::lock_guard<std::mutex> lk(j->mu);
-        j->ok = ok;
-        j->why = std::move(why);
-        j->code = std::move(code);
-        j->done = true;
-        j->cv.notify_all();
-        return;
-    }
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, j->src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-        why = "hiprtcCreateProgram failed";
-    } else {
-        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-        const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
-        size_t cs = 0;
-        if (r != HIPRTC_SUCCESS) {
-            size_t ls = 0;
-            (void)hiprtcGetProgramLogSize(prog, &ls);
-            std::string log(ls, '\0');
-            if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
-            why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
-        } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
-            why = "hiprtc produced no code";
-        } else {
-            code.resize(cs);
-            (void)hiprtcGetCode(prog, code.data());
+    const bool spawned = !helper.empty() && rtc_spawn(helper, j->src, ok, why, code);
+    std::string from = spawned ? "helper" : "inproc";
+    if (!spawned || inproc_rtc_differs()) {
+        bool ok2 = false;
+        std::string why2;
+        std::vector<char> code2;
+        rtc_inproc(j->src, ok2, why2, code2);
+        const uint32_t v1 = ok ? code_vgprs(code) : 0u, v2 = ok2 ? code_vgprs(code2) : 0u;
+        if (ok2 && (!ok || (v2 && v1 && v2 < v1))) {
             ok = true;
+            code = std::move(code2);
+            why.clear();
+            from = "inproc";
+        } else if (!ok) {
+            why = why2;
         }
-        (void)hiprtcDestroyProgram(&prog);
     }
+    if (ok) why = from; // which compiler's module (mk_net_plan)
     std::lock_guard<std::mutex> lk(j->mu);
     j->ok = ok;
     j->why = std::move(why);
@@ -2061,6 +2106,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
             return false;
         }
         J.code = std::move(job->code);
+        J.rtc = job->why; // the compiler whose module this is (hiprtc_run)
     }
     if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded
         if (FILE *f = std::fopen(d, "wb")) {
@@ -2993,7 +3039,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     std::string s;
     if (t == mk::TIER_NATIVE) {
         char tail[160];
-        snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs",
+        snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs rtc=%s",
                  sc->jit.shape == mk::JIT_MACHINE ? "machine"
                  : sc->jit.heavy                  ? (sc->jit.lds ? "stream-heavy-lds"
                                                      : sc->jit.lds_n ? "stream-heavy-split"
@@ -3003,7 +3049,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                  : sc->jit.pool     ? ("-k" + std::to_string(sc->jit.pool)).c_str()
                                     : "",
                  sc->jit.src_bytes,
-                 sc->jit.code.size(), sc->jit.compile_s);
+                 sc->jit.code.size(), sc->jit.compile_s, sc->jit.rtc.c_str());
         s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
     } else {
         const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
