@@ -1898,6 +1898,7 @@ struct HiprtcJob {
     std::mutex mu;
     std::condition_variable cv;
     bool done = false, ok = false;
+    bool heavy = false; // a heavy stream module: worth the helper's compile too (hiprtc_run)
     std::string why;
     std::vector<char> code;
 };
@@ -2028,12 +2029,15 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     bool ok = false;
     std::string why;
     std::vector<char> code;
-    // The helper's module (this ROCm's compiler); where the in-process
-    // compiler is another one, its module too, and the one whose kernel
-    // needs fewer VGPRs is kept -- each compiler wins some networks (C4
+    // Heavy modules: the helper's module (this ROCm's compiler); where the
+    // in-process compiler is another one, its module too, and the one whose
+    // kernel needs fewer VGPRs is kept -- each compiler wins some networks (C4
     // D=64: 58 vs 94 VGPRs, 59 vs 72 us, for the in-process one; D=256: 75
     // vs 132 VGPRs, 191 vs 319 us, for the helper's).
-    const std::string helper = rtc_helper();
+    // Only heavy stream modules, where the two compilers' register use
+    // differs most, pay for a second compile and a helper process (≈0.3 s to
+    // start); the others compile in process.
+    const std::string helper = j->heavy ? rtc_helper() : std::string();
     const bool spawned = !helper.empty() && rtc_spawn(helper, j->src, ok, why, code);
     std::string from = spawned ? "helper" : "inproc";
     if (!spawned || inproc_rtc_differs()) {
@@ -2089,6 +2093,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
+    job->heavy = J.heavy;
     J.src_bytes = job->src.size();
     std::thread(hiprtc_run, job).detach();
     {
