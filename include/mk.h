@@ -45,6 +45,7 @@ extern "C" {
 #define MK_ST_STACK_OVERFLOW 3 /* a PUSH exceeded stack_cap (reference stacks are unbounded)  */
 #define MK_ST_OUTPUT_STOP 4    /* stopped at the first OUT (MK_FLAG_STOP_ON_OUTPUT)           */
 #define MK_ST_REMOTE_WAIT 5    /* session call parked on remote peers / inbound RPCs (row f4)  */
+#define MK_ST_CALL_OPEN 6      /* session: a call is still open; this new one did nothing      */
 #define MK_ST_REASON_MASK 0x0f
 #define MK_ST_HAS_OUTPUT 0x10  /* lane produced a /compute result                              */
 
@@ -166,12 +167,24 @@ int mk_compute_device(mk_net *net, int device, const mk_input *in, size_t n, int
  * post-/run state; one compute call performs one /compute (master.go:
  * 216-219) on every session at once: deposit in[i] once inChan is empty,
  * run until outChan holds a value and take it.  status[i] is
- * MK_ST_HAS_OUTPUT with out[i] the value, or the reason the call could not
- * complete (MK_ST_QUIESCENT: the reference's handler would block forever;
- * MK_ST_BUDGET: opts->budget retired instructions in this call;
- * MK_ST_STACK_OVERFLOW); such a session stays ended (same status, no
- * output) until mk_session_reset.  steps[i] (nullable): instructions retired
- * in this call.  The mk_net must outlive its sessions. */
+ * MK_ST_HAS_OUTPUT with out[i] the value, or why the call has no result:
+ *   MK_ST_BUDGET: this slice of the call retired opts->budget instructions.
+ *     The call stays OPEN -- the reference's handler keeps waiting while its
+ *     nodes run on (program.go:80-92) -- and mk_session_step(in = NULL)
+ *     continues it with a fresh budget; mk_session_cancel abandons it.
+ *   MK_ST_QUIESCENT: nothing can change without another input (the
+ *     reference's handler would block forever).  The call closes; the
+ *     instance keeps its state and takes the next call's input.
+ *   MK_ST_STACK_OVERFLOW: a PUSH beyond stack_cap (the reference's stacks
+ *     are unbounded): the session stays ended (same status, no output) until
+ *     mk_session_reset.
+ *   MK_ST_CALL_OPEN: the session already had an open call; this call did
+ *     nothing and its input was not taken.  The host calls return MK_EBUSY
+ *     when any session had a call open as the launch began (a burst's later
+ *     calls behind a call that stayed open in the same launch report it too,
+ *     without MK_EBUSY).
+ * steps[i] (nullable): instructions retired by the call so far, over all
+ * its slices (mod 2^32).  The mk_net must outlive its sessions. */
 typedef struct mk_session mk_session;
 
 int mk_session_create(mk_net *net, int device, size_t n, const mk_opts *opts, mk_session **out);
@@ -205,7 +218,9 @@ int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out
  *   - serves the peers' RPCs to this instance's nodes: Program.Send into a
  *     local port (mk_session_port_put, MK_EBUSY while full: program.go:163),
  *     Stack.Push / Stack.Pop on a local stack (mk_session_stack_push / _pop,
- *     MK_EBUSY while empty: stack.go:133-155);
+ *     MK_EBUSY while empty: stack.go:133-155), and Master.GetInput /
+ *     SendOutput on the master's channels (mk_session_input_take /
+ *     _output_put);
  *   - resumes the call (mk_session_step with in = NULL).
  * All of these are ordered on the session's stream and synchronous. */
 #define MK_REMOTE_SEND 0
@@ -220,18 +235,32 @@ typedef struct {
 } mk_remote_req;
 
 /* One call step on every session: a new /compute call with in[i] (host
- * arrays), or, with in == NULL, resume each session's parked call. */
+ * arrays), or, with in == NULL, resume each session's open call (parked on
+ * peers, or out of budget); sessions without one report status 0. */
 int mk_session_step(mk_session *s, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps);
 int mk_session_remote_poll(mk_session *s, size_t inst, mk_remote_req *reqs, int max, int *count);
 int mk_session_remote_done(mk_session *s, size_t inst, uint32_t node, int32_t value);
 int mk_session_port_put(mk_session *s, size_t inst, uint32_t node, uint32_t reg, int32_t value);
 int mk_session_stack_push(mk_session *s, size_t inst, uint32_t stack, int32_t value);
 int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *value);
+/* The master's side for remote program nodes that do IN / OUT: their
+ * Master.GetInput takes from this instance's inChan (master.go:233-242;
+ * MK_EBUSY while it is empty and no open call holds an input to deposit --
+ * the reference's receive blocks), their Master.SendOutput deposits into its
+ * outChan (master.go:245-249; MK_EBUSY while full).  The open call takes
+ * that output when it resumes. */
+int mk_session_input_take(mk_session *s, size_t inst, int32_t *value);
+int mk_session_output_put(mk_session *s, size_t inst, int32_t value);
 
 /* Kind (MK_NODE_*) and index of a node by name: program and stack nodes in
  * sorted-name order (the canonical schedule), remote peers in declaration
  * order. */
 int mk_net_node_index(const mk_net *net, const char *name, int *kind, int *index);
+
+/* Abandon every session's open call (the master answered it 504).  What it
+ * set in motion stays: an input it deposited in inChan, the nodes' progress;
+ * an input not deposited yet is dropped.  Synchronous. */
+int mk_session_cancel(mk_session *s);
 
 /* /reset (master.go:126-143): every session back to the initial state. */
 int mk_session_reset(mk_session *s);

@@ -38,6 +38,7 @@ const (
 	StackOverflow = C.MK_ST_STACK_OVERFLOW
 	OutputStop    = C.MK_ST_OUTPUT_STOP
 	RemoteWait    = C.MK_ST_REMOTE_WAIT
+	CallOpen      = C.MK_ST_CALL_OPEN
 	HasOutput     = C.MK_ST_HAS_OUTPUT
 )
 
@@ -169,6 +170,15 @@ func (s *Sessions) Compute(in []int) (*Result, error) {
 	return r, nil
 }
 
+// Cancel abandons every instance's open call (mk_session_cancel): the
+// master answered it 504.  What the call set in motion stays.
+func (s *Sessions) Cancel() error {
+	if rc := C.mk_session_cancel(s.s); rc != C.MK_OK {
+		return fmt.Errorf("mk_session_cancel: %d", int(rc))
+	}
+	return nil
+}
+
 // Reset is /reset for every instance (master.go:126-143).
 func (s *Sessions) Reset() error {
 	if rc := C.mk_session_reset(s.s); rc != C.MK_OK {
@@ -210,8 +220,9 @@ func (s *Sessions) ComputeSeq(in []int) (*Result, error) {
 	return r, nil
 }
 
-// Step starts a call on instance 0..n-1 (in != nil) or resumes the parked
-// calls of a mixed deployment (in == nil) -- mk_session_step.
+// Step starts a call on instance 0..n-1 (in != nil) or resumes the open
+// calls (in == nil): parked on the peers of a mixed deployment, or out of
+// their budget slice (status Budget) -- mk_session_step.
 func (s *Sessions) Step(in []int) (*Result, error) {
 	r := &Result{Out: make([]int32, s.n), Status: make([]uint8, s.n), Steps: make([]uint32, s.n)}
 	var p *C.int64_t

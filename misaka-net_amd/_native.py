@@ -27,6 +27,7 @@ MK_ST_BUDGET = 2
 MK_ST_STACK_OVERFLOW = 3
 MK_ST_OUTPUT_STOP = 4
 MK_ST_REMOTE_WAIT = 5
+MK_ST_CALL_OPEN = 6
 MK_ST_REASON_MASK = 0x0F
 MK_ST_HAS_OUTPUT = 0x10
 
@@ -121,6 +122,7 @@ SIGNATURES = {
     "mk_session_compute_seq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_compute_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_reset": (C.c_int, [C.c_void_p]),
+    "mk_session_cancel": (C.c_int, [C.c_void_p]),
     "mk_session_free": (None, [C.c_void_p]),
     "mk_generate_inputs_device": (
         C.c_int,
@@ -141,6 +143,8 @@ SIGNATURES = {
     "mk_session_port_put": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_int32]),
     "mk_session_stack_push": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_int32]),
     "mk_session_stack_pop": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.POINTER(C.c_int32)]),
+    "mk_session_input_take": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_int32)]),
+    "mk_session_output_put": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int32]),
     "mk_net_node_index": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mk_trace_lane": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.POINTER(mk_opts), C.c_void_p, C.c_uint32,
                                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]),

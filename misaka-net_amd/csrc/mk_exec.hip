@@ -912,10 +912,11 @@ __global__ void __launch_bounds__(B) tis_sched_tile(const DOp *__restrict__ code
 // session, one thread each (oracle: tis_oracle.c session_call):
 //   loop: deposit the input once inChan is empty (m.inChan <- v, :216);
 //         take outChan's value once the input is deposited (:219) -> result;
-//         end the call at the per-call budget; run one round; a stack
-//         overflow or a round without change ends it.
-// A call without a result ends the session (the reference handler would
-// block forever): it reports that reason now and on every later call.
+//         end the slice at the budget; run one round; a stack overflow or a
+//         round without change ends the call.
+// A call whose slice reaches the budget stays open (MK_ST_BUDGET) and a
+// resume launch continues it; a round without change closes it without a
+// result and the instance lives on; a stack overflow ends the session.
 // Ports are staged in LDS for the call; stack entries stay in HBM.
 // ------------------------------------------------------------------------
 struct SessParams {
@@ -996,14 +997,21 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     // from one to the next (a burst of requests on one instance, one launch)
     for (uint32_t call = 0; call < p.ncalls; ++call) {
     const uint64_t ci = (uint64_t)call * n + gid;
-    // a parked call (mixed networks) resumes with its input (deposited or not) and step count
-    const bool resumed = p.resume && live && ((io >> 3) & 1u);
+    // io bit 3: a call is open (it parked on peers or ran out of its slice's
+    // budget); bit 2: its input is not deposited yet (held in pin).  A resume
+    // continues it with its input and step count; a new call while one is
+    // open does nothing and reports MK_ST_CALL_OPEN (tis_oracle.c session_step)
+    const bool open = live && ((io >> 3) & 1u);
+    const bool resumed = p.resume && open;
+    const bool ran = live && dead == 0 && (p.resume ? resumed : !open);
     const int32_t x = !live ? 0 : resumed ? p.pin[gid] : (int32_t)p.in[ci]; // int32(v) at GetInput (master.go:237)
-    bool active = live && dead == 0 && (!p.resume || resumed), got = false;
+    bool active = ran, got = false;
     bool deposited = resumed && !((io >> 2) & 1u);
     int32_t result = 0;
     uint32_t steps = resumed ? p.csteps[gid] : 0u;
-    bool parked = false;
+    const uint32_t slice0 = steps;
+    bool parked = false; // the call stays open
+    uint32_t reason = 0;
 
     for (;;) {
         if (active) {
@@ -1017,8 +1025,9 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
                 result = out_val;
                 got = true;
                 active = false;
-            } else if (steps >= p.budget) {
-                dead = MK_ST_BUDGET;
+            } else if (steps - slice0 >= p.budget) { // this slice is spent; the call stays open
+                reason = MK_ST_BUDGET;
+                parked = true;
                 active = false;
             }
         }
@@ -1174,25 +1183,29 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
             }
         }
         if (active) {
-            if (over) {
-                dead = MK_ST_STACK_OVERFLOW;
+            if (over) { // stack_cap (ours; the reference's stacks are unbounded) ends the session
+                dead = reason = MK_ST_STACK_OVERFLOW;
                 active = false;
             } else if (!changed) {
-                if (p.mixed) parked = true; // waits on peers or on the host's inbound RPCs
-                else dead = MK_ST_QUIESCENT;
+                // waits on peers or on the host's inbound RPCs: stays open;
+                // otherwise nothing can change without another input -- the
+                // call closes and the instance lives on
+                if (p.mixed) parked = true, reason = MK_ST_REMOTE_WAIT;
+                else reason = MK_ST_QUIESCENT;
                 active = false;
             }
         }
     }
     if (live) {
         p.out[ci] = got ? result : 0;
-        p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : parked ? MK_ST_REMOTE_WAIT : dead);
-        if (p.steps) p.steps[ci] = steps;
-        // the call stays open while parked: input not yet deposited (bit 2), call open (bit 3)
-        io = (io & ~0xCu) | (parked && !deposited ? 4u : 0u) | (parked ? 8u : 0u);
-        if (parked) {
-            p.pin[gid] = x;
-            p.csteps[gid] = steps;
+        p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : ran ? reason : dead ? dead : open && !p.resume ? MK_ST_CALL_OPEN : 0u);
+        if (p.steps) p.steps[ci] = ran ? steps : 0u;
+        if (ran) { // the call stays open while parked: input not yet deposited (bit 2), call open (bit 3)
+            io = (io & ~0xCu) | (parked && !deposited ? 4u : 0u) | (parked ? 8u : 0u);
+            if (parked) {
+                p.pin[gid] = x;
+                p.csteps[gid] = steps;
+            }
         }
     }
     } // calls
@@ -1221,6 +1234,14 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (io & 0xCu) | (dead << 4);
     p.in_val[gid] = in_val;
     p.out_val[gid] = out_val;
+}
+
+// mk_session_cancel: abandon every open call (io bits 2-3); the state the
+// call left behind -- its input if deposited, the nodes' progress -- stays.
+__global__ void __launch_bounds__(kBlock) tis_session_cancel(uint32_t *io, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) io[i] &= ~0xCu;
 }
 
 // ---- input order for the machine shape (tier 3) -----------------------------
@@ -2773,6 +2794,11 @@ int session_host_calls(mk_session *s, const int64_t *in, size_t ncalls, int32_t 
     memcpy(out, hb + a8, m * 4);
     memcpy(status, hb + a8 + a4 + a4, m);
     if (steps) memcpy(steps, hb + a8 + a4, m * 4);
+    // a session that had a call open when this launch began did nothing
+    // (MK_ST_CALL_OPEN): resume or cancel that call first
+    if (!resume)
+        for (size_t i = 0; i < s->n; i++)
+            if (status[i] == MK_ST_CALL_OPEN) return MK_EBUSY;
     return MK_OK;
 }
 
@@ -2883,6 +2909,36 @@ int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *va
     return mk::sput(s, s->p.sdepth + (uint64_t)stack * s->n + inst, (int32_t)(d - 1));
 }
 
+int mk_session_input_take(mk_session *s, size_t inst, int32_t *value)
+{
+    if (!s || !value || inst >= s->n) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    uint32_t io = 0;
+    int rc = mk::sget(s, s->p.io + inst, io);
+    if (rc) return rc;
+    if (io & 1u) { // <-m.inChan (master.go:235)
+        if ((rc = mk::sget(s, s->p.in_val + inst, *value))) return rc;
+        return mk::sput(s, s->p.io + inst, io & ~1u);
+    }
+    if ((io & 0xCu) == 0xCu) // the open call is still waiting to deposit (m.inChan <- v, :216): hand it over
+        return (rc = mk::sget(s, s->p.pin + inst, *value)) ? rc : mk::sput(s, s->p.io + inst, io & ~4u);
+    return MK_EBUSY; // GetInput blocks while inChan is empty
+}
+
+int mk_session_output_put(mk_session *s, size_t inst, int32_t value)
+{
+    if (!s || inst >= s->n) return MK_EINVAL;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    uint32_t io = 0;
+    int rc = mk::sget(s, s->p.io + inst, io);
+    if (rc) return rc;
+    if (io & 2u) return MK_EBUSY; // m.outChan <- v blocks while full (master.go:246)
+    if ((rc = mk::sput(s, s->p.out_val + inst, value))) return rc;
+    return mk::sput(s, s->p.io + inst, io | 2u);
+}
+
 int mk_net_node_index(const mk_net *h, const char *name, int *kind, int *index)
 {
     if (!h || !name || !kind || !index) return MK_EINVAL;
@@ -2894,6 +2950,22 @@ int mk_net_node_index(const mk_net *h, const char *name, int *kind, int *index)
     for (size_t i = 0; i < N.remote_names.size(); i++)
         if (N.remote_names[i] == name) { *kind = N.remote_kinds[i]; *index = (int)i; return MK_OK; }
     return MK_EINVAL;
+}
+
+int mk_session_cancel(mk_session *s)
+{
+    if (!s) return MK_EINVAL;
+    if (s->n == 0) return MK_OK;
+    std::lock_guard<std::mutex> lk(s->mu);
+    mk::DeviceGuard g(s->device);
+    uint32_t *io = s->p.io;
+    uint64_t n = s->n;
+    void *args[] = {(void *)&io, (void *)&n};
+    const uint64_t blocks = (n + mk::kBlock - 1) / mk::kBlock;
+    if (hipLaunchKernel(reinterpret_cast<void *>(&mk::tis_session_cancel), dim3((unsigned)blocks), dim3(mk::kBlock),
+                        args, 0, s->stream) != hipSuccess)
+        return MK_EDEVICE;
+    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 
 void mk_session_free(mk_session *s) { delete s; }

@@ -36,12 +36,18 @@ Deliberate differences (DESIGN.md / INTEGRATION.md):
     the channels.  ``wire_timeout`` bounds the wait (504), the reference has
     none.
   * a /compute whose network produces no output answers 504 "network
-    produced no output" instead of hanging forever.
+    produced no output" instead of hanging forever: at once when nothing
+    can change without another input (the instance keeps its state and
+    serves the next call), or, stateful, after ``call_timeout`` seconds of
+    resuming a call that keeps running (it is abandoned; what it deposited
+    stays).  The reference's abandoned handler would instead stay blocked on
+    outChan and take the next output (master.go:219).
 """
 from __future__ import annotations
 
 import json
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Mapping, Optional
 from urllib.parse import unquote_to_bytes
@@ -164,7 +170,8 @@ class MasterNode:
 
     def __init__(self, node_info: Mapping[str, Mapping], programs: Optional[Mapping[str, str]] = None,
                  name: str = "last_order", devices=None, budget=None, stack_cap=None, stateful: bool = True,
-                 wire=None, wire_timeout: Optional[float] = 30.0, max_batch: int = 65536):
+                 wire=None, wire_timeout: Optional[float] = 30.0, max_batch: int = 65536,
+                 call_timeout: Optional[float] = 30.0):
         self.node_info = {k: dict(v) for k, v in node_info.items()}
         self.name = name
         self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
@@ -184,6 +191,10 @@ class MasterNode:
         self.stateful = stateful
         self._sess = None
         self.wire, self.wire_timeout = wire, wire_timeout
+        # stateful mode: how long a call that outlives its budget slice is
+        # resumed before it is answered 504 and abandoned (the reference's
+        # handler waits forever, master.go:219)
+        self.call_timeout = call_timeout
         self.coalescer = Coalescer(self._run_batch, max_batch)
 
     # -- network handle ------------------------------------------------------
@@ -220,11 +231,49 @@ class MasterNode:
         independent lanes (stateless); one executor launch either way."""
         with self._lock:
             if self.stateful:
-                r = self.session().compute_seq(np.asarray(vals, dtype=np.int64), steps=False)
-            else:
-                r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
-                                                 stack_cap=self.stack_cap, devices=self.devices, steps=False)
+                return [(h, o) for h, o, _ in self._run_stateful(vals)]
+            r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
+                                             stack_cap=self.stack_cap, devices=self.devices, steps=False)
         return [(bool(int(st) & N.MK_ST_HAS_OUTPUT), int(o)) for o, st in zip(r.out.tolist(), r.status.tolist())]
+
+    def _run_stateful(self, vals):
+        """Sequential /compute calls on the one instance -> [(has_output,
+        value, status)].  Caller holds self._lock.  A call that spends its
+        budget slice stays open (the reference's nodes never give up,
+        program.go:80-92): it is resumed until it has its output, closes, or
+        ``call_timeout`` passes (then 504, and the call is abandoned: the
+        instance lives on).  The burst's later calls, which did not run
+        behind it (MK_ST_CALL_OPEN), go in the next launch."""
+        sess = self.session()
+        res: list = []
+        while len(res) < len(vals):
+            r = sess.compute_seq(np.asarray(vals[len(res):], dtype=np.int64), steps=False, busy_ok=True)
+            for o, st in zip(r.out.tolist(), r.status.tolist()):
+                reason = st & N.MK_ST_REASON_MASK
+                if st & N.MK_ST_HAS_OUTPUT:
+                    res.append((True, o, st))
+                elif reason == N.MK_ST_BUDGET:
+                    res.append(self._finish_open_call(sess))
+                    break
+                elif reason == N.MK_ST_CALL_OPEN:  # left open before this burst
+                    sess.cancel()
+                    break
+                else:  # quiescent (the call closed, the instance lives on) or stack overflow
+                    res.append((False, 0, st))
+        return res
+
+    def _finish_open_call(self, sess):
+        deadline = None if self.call_timeout is None else time.monotonic() + self.call_timeout
+        while True:
+            r = sess.resume(steps=False)
+            o, st = int(r.out[0]), int(r.status[0])
+            if st & N.MK_ST_HAS_OUTPUT:
+                return True, o, st
+            if (st & N.MK_ST_REASON_MASK) != N.MK_ST_BUDGET:
+                return False, 0, st
+            if deadline is not None and time.monotonic() >= deadline:
+                sess.cancel()
+                return False, 0, st
 
     def _call(self, v: int):
         """One /compute: (has_output, value)."""
@@ -358,9 +407,9 @@ class MasterNode:
         except (ValueError, TypeError, AttributeError):
             return http_error("cannot parse value", 400)
         with self._lock:
-            if self.stateful:  # sequential /compute calls on the one instance, one launch
-                r = self.session().compute_seq(np.asarray(vals, dtype=np.int64), steps=False)
-                outs, sts = r.out.tolist(), r.status.tolist()
+            if self.stateful:  # sequential /compute calls on the one instance
+                got = self._run_stateful(vals)
+                outs, sts = [g[1] for g in got], [g[2] for g in got]
             else:
                 r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
                                                  stack_cap=self.stack_cap, devices=self.devices, steps=False)

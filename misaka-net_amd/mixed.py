@@ -20,9 +20,16 @@ reference's processes talk to:
     per call as the reference dials per operation -- reports completions to
     the session, waits for a completion or an inbound RPC, and resumes.
 
-Not covered: IN / OUT on remote nodes (the master's inChan / outChan live in
-the GPU instance; a remote node's Master.GetInput would need them served
-from it), and several GPU instances sharing one set of peers.
+  * for the network's master node (kind ``master``) it serves
+    ``grpc.Master/GetInput`` and ``SendOutput`` (master.go:233-249) on the
+    GPU instance's inChan / outChan, so remote program nodes can do IN / OUT.
+
+Calls are serialised (the reference's capacity-1 inChan/outChan serve one
+/compute at a time, master.go:216-219).  A call that spends its budget
+slice stays open and is resumed; a call still open at its timeout is
+abandoned (mk_session_cancel), so the next call starts cleanly.
+
+Not covered: several GPU instances sharing one set of peers.
 """
 from __future__ import annotations
 
@@ -52,6 +59,7 @@ class MixedHost:
         self.rpc_timeout = rpc_timeout
         self.remote_names = remote  # MK_NODE_REMOTE_* in declaration order = the C index
         self._mu = threading.Lock()  # the session: steps and state edits
+        self._call_mu = threading.Lock()  # one /compute call at a time, start to end
         self._cv = threading.Condition()
         self._gen = 0  # bumped by every inbound deposit and outbound completion
         self._inflight: set = set()
@@ -71,6 +79,14 @@ class MixedHost:
                     "Pop": grpc.unary_unary_rpc_method_handler(self._pop_handler(s.name),
                                                                request_deserializer=wire.decode_empty,
                                                                response_serializer=wire.encode_value)}, host)
+            elif s.kind == "master":
+                self._serve(s.name, "Master", {
+                    "GetInput": grpc.unary_unary_rpc_method_handler(self._get_input,
+                                                                    request_deserializer=wire.decode_empty,
+                                                                    response_serializer=wire.encode_value),
+                    "SendOutput": grpc.unary_unary_rpc_method_handler(self._send_output,
+                                                                      request_deserializer=wire.decode_value,
+                                                                      response_serializer=wire.encode_empty)}, host)
 
     # ---- plumbing ---------------------------------------------------------------
     def _serve(self, name, service, handlers, host):
@@ -168,6 +184,33 @@ class MixedHost:
 
         return pop
 
+    def _get_input(self, _req, context):  # Master.GetInput (master.go:233-242): blocks while inChan is empty
+        def attempt():
+            v = C.c_int32()
+            with self._mu:
+                rc = N.lib().mk_session_input_take(self.sess._h, 0, C.byref(v))
+            if rc == N.MK_EBUSY:
+                raise _Busy()
+            if rc != N.MK_OK:
+                context.abort(grpc.StatusCode.INTERNAL, f"{N.ERROR_NAMES.get(rc, rc)}: mk_session_input_take")
+            self._event()
+            return v.value
+
+        return self._blocking(attempt, context)
+
+    def _send_output(self, value, context):  # Master.SendOutput (master.go:245-249): blocks while outChan is full
+        def attempt():
+            with self._mu:
+                rc = N.lib().mk_session_output_put(self.sess._h, 0, value)
+            if rc == N.MK_EBUSY:
+                raise _Busy()
+            if rc != N.MK_OK:
+                context.abort(grpc.StatusCode.INTERNAL, f"{N.ERROR_NAMES.get(rc, rc)}: mk_session_output_put")
+            self._event()
+            return wire.EMPTY
+
+        return self._blocking(attempt, context)
+
     # ---- outbound RPCs of the GPU instance's nodes ----------------------------------
     def _rpc(self, req):
         target = self.peers[self.remote_names[req.remote]]
@@ -227,20 +270,32 @@ class MixedHost:
 
     # ---- /compute ----------------------------------------------------------------------
     def compute(self, x: int, timeout: Optional[float] = 60.0):
-        """One /compute on the GPU instance: (has_output, value, status)."""
-        deadline = None if timeout is None else time.monotonic() + timeout
-        st, out, gen = self._step(x)
-        while True:
-            if st & N.MK_ST_HAS_OUTPUT:
-                return True, out, st
-            if (st & N.MK_ST_REASON_MASK) != N.MK_ST_REMOTE_WAIT:
-                return False, 0, st
-            self._start_requests()
-            left = None if deadline is None else deadline - time.monotonic()
-            if left is not None and left <= 0:
-                return False, 0, st
-            self._wait_event(gen, min(0.5, left) if left is not None else 0.5)
-            st, out, gen = self._step(None)
+        """One /compute on the GPU instance: (has_output, value, status).
+        A call parked on peers (MK_ST_REMOTE_WAIT) or out of its budget slice
+        (MK_ST_BUDGET) is resumed until it has its output, closes, or
+        ``timeout`` passes; then it is abandoned and the instance lives on."""
+        with self._call_mu:
+            deadline = None if timeout is None else time.monotonic() + timeout
+            done = False
+            try:
+                st, out, gen = self._step(x)
+                while True:
+                    reason = st & N.MK_ST_REASON_MASK
+                    if st & N.MK_ST_HAS_OUTPUT or reason not in (N.MK_ST_REMOTE_WAIT, N.MK_ST_BUDGET):
+                        done = True
+                        return bool(st & N.MK_ST_HAS_OUTPUT), out if st & N.MK_ST_HAS_OUTPUT else 0, st
+                    left = None if deadline is None else deadline - time.monotonic()
+                    if left is not None and left <= 0:
+                        return False, 0, st
+                    if reason == N.MK_ST_REMOTE_WAIT:
+                        self._start_requests()
+                        self._wait_event(gen, min(0.5, left) if left is not None else 0.5)
+                    st, out, gen = self._step(None)
+            finally:
+                if not done and not self._closed:  # timed out (or failed) with the call open
+                    with self._mu:
+                        N.check(N.lib().mk_session_cancel(self.sess._h), "mk_session_cancel")
+                    self._event()
 
     def close(self):
         self._closed = True

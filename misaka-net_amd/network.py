@@ -288,24 +288,43 @@ class SessionSet:
         N.check(N.lib().mk_session_create(net.handle, device, n, C.byref(o), C.byref(h)), "mk_session_create")
         self._h, self._net, self.n, self.device = h, net, n, device
 
-    def compute(self, values, *, steps=True) -> BatchResult:
-        """One /compute call per instance: ``values[i]`` goes to instance i."""
+    def compute(self, values, *, steps=True, busy_ok=False) -> BatchResult:
+        """One /compute call per instance: ``values[i]`` goes to instance i.
+
+        A call whose budget slice runs out stays open (status MK_ST_BUDGET):
+        :meth:`resume` continues it, :meth:`cancel` abandons it.  While one is
+        open a new call on that instance does nothing (MK_ST_CALL_OPEN) and
+        this raises MkError(MK_EBUSY) unless ``busy_ok``."""
         v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
         if v.size != self.n:
             raise ValueError(f"expected {self.n} values, got {v.size}")
+        return self._step(v.ctypes.data_as(C.c_void_p), steps, busy_ok, "mk_session_compute")
+
+    def resume(self, *, steps=True) -> BatchResult:
+        """One more budget slice of every instance's open call (instances
+        without one report status 0) -- mk_session_step(in = NULL)."""
+        return self._step(None, steps, False, "mk_session_step")
+
+    def _step(self, vp, steps, busy_ok, what) -> BatchResult:
         out = np.zeros(self.n, np.int32)
         st = np.zeros(self.n, np.uint8)
         sp = np.zeros(self.n, np.uint32) if steps else None
-        N.check(N.lib().mk_session_compute(self._h, v.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
-                                           st.ctypes.data_as(C.c_void_p),
-                                           sp.ctypes.data_as(C.c_void_p) if sp is not None else None),
-                "mk_session_compute")
+        rc = N.lib().mk_session_step(self._h, vp, out.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p),
+                                     sp.ctypes.data_as(C.c_void_p) if sp is not None else None)
+        if not (busy_ok and rc == N.MK_EBUSY):
+            N.check(rc, what)
         return BatchResult(out, st, sp)
 
-    def compute_seq(self, values, *, steps=True) -> BatchResult:
+    def cancel(self):
+        """Abandon every instance's open call (mk_session_cancel)."""
+        N.check(N.lib().mk_session_cancel(self._h), "mk_session_cancel")
+
+    def compute_seq(self, values, *, steps=True, busy_ok=False) -> BatchResult:
         """Sequential /compute calls in one launch: ``values`` has shape
         (ncalls, n) -- row c is call c on every instance -- or, for n == 1,
-        a flat list of the calls.  Results have the shape of ``values``."""
+        a flat list of the calls.  Results have the shape of ``values``.  A
+        call that stays open (MK_ST_BUDGET) makes the instance's later calls
+        of the burst report MK_ST_CALL_OPEN without running."""
         v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
         shape = v.shape
         if v.ndim == 1 and self.n == 1:
@@ -317,10 +336,11 @@ class SessionSet:
         st = np.zeros(v.shape, np.uint8)
         sp = np.zeros(v.shape, np.uint32) if steps else None
         if m:
-            N.check(N.lib().mk_session_compute_seq(self._h, v.ctypes.data_as(C.c_void_p), m,
-                                                   out.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p),
-                                                   sp.ctypes.data_as(C.c_void_p) if sp is not None else None),
-                    "mk_session_compute_seq")
+            rc = N.lib().mk_session_compute_seq(self._h, v.ctypes.data_as(C.c_void_p), m,
+                                                out.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p),
+                                                sp.ctypes.data_as(C.c_void_p) if sp is not None else None)
+            if not (busy_ok and rc == N.MK_EBUSY):
+                N.check(rc, "mk_session_compute_seq")
         return BatchResult(out.reshape(shape), st.reshape(shape), sp.reshape(shape) if sp is not None else None)
 
     def compute_device(self, in_ptr, out_ptr, status_ptr, steps_ptr=None, *, stream=None):

@@ -18,16 +18,28 @@ SRC = os.path.join(HERE, "tis_oracle.c")
 LIB = os.path.join(HERE, "build", "liboracle_tis.so")
 
 ST_QUIESCENT, ST_BUDGET, ST_STACK_OVERFLOW, ST_OUTPUT_STOP, ST_HAS_OUTPUT = 1, 2, 3, 4, 0x10
+ST_CALL_OPEN = 6
 KIND = {"program": 0, "stack": 1}
 
 
 def build(force: bool = False) -> str:
     """Compile the oracle with gcc (no GPU needed)."""
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+    import hashlib
+
+    with open(SRC, "rb") as f:
+        stamp = hashlib.sha256(f.read()).hexdigest()  # content, not mtime: the tree travels to the GPU box
+    try:
+        with open(LIB + ".stamp") as f:
+            fresh = os.path.exists(LIB) and f.read().strip() == stamp
+    except OSError:
+        fresh = False
+    if force or not fresh:
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        subprocess.check_call(
-            ["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-pthread", "-o", LIB, SRC]
-        )
+        tmp = f"{LIB}.tmp{os.getpid()}"
+        subprocess.check_call(["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-pthread", "-o", tmp, SRC])
+        os.replace(tmp, LIB)
+        with open(LIB + ".stamp", "w") as f:
+            f.write(stamp + "\n")
     return LIB
 
 
@@ -69,6 +81,7 @@ def lib():
         h.orc_sessions_new.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
         h.orc_sessions_free.argtypes = [C.c_void_p]
         h.orc_sessions_reset.argtypes = [C.c_void_p]
+        h.orc_sessions_cancel.argtypes = [C.c_void_p]
         h.orc_sessions_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                            C.c_int]
         h.orc_go_atoi.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64)]
@@ -191,16 +204,29 @@ class OracleSessions:
         lib().orc_sessions_reset(self._h)
 
     def compute(self, values, *, budget: Optional[int] = None, threads: int = 1):
-        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
-        assert v.size == self.n
+        """One /compute call per instance (``values`` None: one more slice
+        of every open call, tis_oracle.c session_step)."""
+        if values is None:
+            vp = None
+        else:
+            v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+            assert v.size == self.n
+            vp = v.ctypes.data_as(C.c_void_p)
         out = np.zeros(self.n, np.int32)
         st = np.zeros(self.n, np.uint8)
         sp = np.zeros(self.n, np.uint32)
-        rc = lib().orc_sessions_compute(self._h, v.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+        rc = lib().orc_sessions_compute(self._h, vp, out.ctypes.data_as(C.c_void_p),
                                         st.ctypes.data_as(C.c_void_p), sp.ctypes.data_as(C.c_void_p),
                                         budget or (1 << 20), threads)
         assert rc == 0
         return out, st, sp
+
+    def resume(self, *, budget: Optional[int] = None, threads: int = 1):
+        return self.compute(None, budget=budget, threads=threads)
+
+    def cancel(self):
+        """Abandon every open call (the master answered it 504)."""
+        lib().orc_sessions_cancel(self._h)
 
 
 def gen_inputs(seed: int, n: int, *, kind: int = 0, mask: int = 0, offset: int = 0) -> np.ndarray:

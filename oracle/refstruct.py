@@ -367,7 +367,7 @@ class MasterEmu:
 class RefStructNet:
     """A running emulated deployment; ``compute(x)`` is one /compute."""
 
-    def __init__(self, nodes: Sequence, *, dial_per_hop: bool = True):
+    def __init__(self, nodes: Sequence, *, dial_per_hop: bool = True, start: bool = True):
         rows = [(n.name, n.kind, n.program) if hasattr(n, "name") else tuple(n) for n in nodes]
         self.stop = threading.Event()
         self.dial_per_hop = dial_per_hop
@@ -388,6 +388,12 @@ class RefStructNet:
             elif kind == "master":
                 self.addr[name] = self.master.addr
         self.threads = [threading.Thread(target=p.loop, daemon=True) for p in self.programs]
+        if start:
+            self.start()
+
+    def start(self):
+        """Start the node loops (``start=False`` lets a test point ``addr`` /
+        ``master_addr`` at other processes' services first)."""
         for t in self.threads:
             t.start()
 
@@ -401,7 +407,8 @@ class RefStructNet:
     def close(self):
         self.stop.set()
         for t in self.threads:
-            t.join(2.0)
+            if t.is_alive():
+                t.join(2.0)
         for x in [self.master] + self.programs + self.stacks:
             x.srv.stop(0)
 

@@ -45,6 +45,7 @@
 #define ST_BUDGET 2
 #define ST_STACK_OVERFLOW 3
 #define ST_OUTPUT_STOP 4
+#define ST_CALL_OPEN 6 /* sessions: a call is still open on this instance (nothing done) */
 #define ST_HAS_OUTPUT 0x10
 
 /* ------------------------------------------------------------------------ */
@@ -632,7 +633,12 @@ typedef struct {
      * each /compute, instead of the single-/compute out_cnt rule */
     int session;
     int out_full;
-    uint8_t dead; /* reason the session ended (0 = alive) */
+    uint8_t dead; /* reason the session ended (0 = alive): a stack overflow */
+    /* the open /compute call: its input (deposited into inChan or not yet),
+     * and the instructions it has retired over its earlier slices */
+    int call_open, call_dep;
+    int64_t call_x;
+    uint32_t call_steps;
 } lane_t;
 
 enum { R_NONE = 0, R_CHANGED = 1, R_RETIRED = 3, R_OVERFLOW = 4 };
@@ -989,12 +995,14 @@ static lane_t *lane_alloc(const orc_net *net, uint32_t cap)
     return ln;
 }
 
-static void lane_free(const orc_net *net, lane_t *ln)
+static void lane_free_n(int nstack, lane_t *ln)
 {
-    for (int i = 0; i < net->nstack; i++)
+    for (int i = 0; i < nstack; i++)
         free(ln->stk[i].v);
     free(ln);
 }
+
+static void lane_free(const orc_net *net, lane_t *ln) { lane_free_n(net->nstack, ln); }
 
 typedef struct {
     const orc_net *net;
@@ -1067,15 +1075,23 @@ int orc_compute_batch(const orc_net *net, const int64_t *in, size_t n, int32_t *
  *     if inChan is empty and the input is not deposited yet: deposit it
  *       (m.inChan <- v blocks while inChan is full, :216);
  *     if it is deposited and outChan holds a value: take it -> the result
- *       (<-m.outChan, :219);
- *     if the call's retired instructions reached the budget: the call ends;
- *     run one round; a stack overflow or a round without change ends it.
- * A call that ends without a result (the reference handler would block
- * forever) ends the session: that call and every later one report the
- * reason without output, until the session is reset. */
+ *       (<-m.outChan, :219), the call closes;
+ *     if this slice of the call retired `budget` instructions: the slice
+ *       ends with ST_BUDGET and the call stays OPEN -- the reference's
+ *       handler is still waiting while its nodes run on (program.go:80-92),
+ *       so session_step(resume) continues it with a fresh slice;
+ *     run one round; a round without change closes the call with
+ *       ST_QUIESCENT (nothing can ever change without another input: the
+ *       reference's handler would block forever; here the call is abandoned
+ *       and the instance stays alive for the next input, an input not yet
+ *       deposited is dropped); a stack overflow (our stack_cap; the
+ *       reference's stacks are unbounded) ends the session until reset.
+ * A new call while one is open does nothing and reports ST_CALL_OPEN; the
+ * host resumes the open call or cancels it (orc_sessions_cancel). */
 typedef struct {
     const orc_net *net;
     size_t n;
+    int nstack; /* freeing never touches net (a garbage collector may free it first) */
     lane_t **lanes;
 } orc_sessions;
 
@@ -1086,31 +1102,48 @@ static void lane_reset_session(const orc_net *net, lane_t *ln)
     ln->session = 1;
     ln->out_full = 0;
     ln->dead = 0;
+    ln->call_open = ln->call_dep = 0;
+    ln->call_x = 0;
+    ln->call_steps = 0;
 }
 
-static uint8_t session_call(const orc_net *net, lane_t *ln, int64_t x, uint32_t budget, int32_t *out,
+/* One slice of a /compute call: a new call with input *x, or (x == NULL)
+ * the open call resumed.  *steps = instructions the call retired so far. */
+static uint8_t session_step(const orc_net *net, lane_t *ln, const int64_t *x, uint32_t budget, int32_t *out,
                             uint32_t *steps)
 {
     *out = 0;
     *steps = 0;
     if (ln->dead)
         return ln->dead;
+    if (!x) {
+        if (!ln->call_open)
+            return 0; /* nothing to resume */
+    } else {
+        if (ln->call_open)
+            return ST_CALL_OPEN;
+        ln->call_open = 1;
+        ln->call_dep = 0;
+        ln->call_x = *x;
+        ln->call_steps = 0;
+    }
     const uint32_t s0 = ln->steps;
-    int deposited = 0;
+    uint8_t st;
     for (;;) {
-        if (!deposited && !ln->in_avail) {
+        if (!ln->call_dep && !ln->in_avail) {
             ln->in_avail = 1;
-            ln->in_val = x;
-            deposited = 1;
+            ln->in_val = ln->call_x;
+            ln->call_dep = 1;
         }
-        if (deposited && ln->out_full) {
+        if (ln->call_dep && ln->out_full) {
             ln->out_full = 0;
             *out = (int32_t)ln->out_val;
-            *steps = ln->steps - s0;
-            return ST_HAS_OUTPUT;
+            st = ST_HAS_OUTPUT;
+            ln->call_open = 0;
+            break;
         }
         if (ln->steps - s0 >= budget) {
-            ln->dead = ST_BUDGET;
+            st = ST_BUDGET; /* the call stays open */
             break;
         }
         int changed = 0, over = 0;
@@ -1123,16 +1156,19 @@ static uint8_t session_call(const orc_net *net, lane_t *ln, int64_t x, uint32_t 
             changed |= r & R_CHANGED;
         }
         if (over) {
-            ln->dead = ST_STACK_OVERFLOW;
+            st = ln->dead = ST_STACK_OVERFLOW;
+            ln->call_open = 0;
             break;
         }
         if (!changed) {
-            ln->dead = ST_QUIESCENT;
+            st = ST_QUIESCENT;
+            ln->call_open = 0;
             break;
         }
     }
-    *steps = ln->steps - s0;
-    return ln->dead;
+    ln->call_steps += ln->steps - s0;
+    *steps = ln->call_steps;
+    return st;
 }
 
 orc_sessions *orc_sessions_new(const orc_net *net, size_t n, uint32_t stack_cap)
@@ -1140,6 +1176,7 @@ orc_sessions *orc_sessions_new(const orc_net *net, size_t n, uint32_t stack_cap)
     orc_sessions *S = (orc_sessions *)calloc(1, sizeof(orc_sessions));
     S->net = net;
     S->n = n;
+    S->nstack = net->nstack;
     S->lanes = (lane_t **)calloc(n ? n : 1, sizeof(lane_t *));
     for (size_t i = 0; i < n; i++) {
         S->lanes[i] = lane_alloc(net, stack_cap);
@@ -1153,7 +1190,7 @@ void orc_sessions_free(orc_sessions *S)
     if (!S)
         return;
     for (size_t i = 0; i < S->n; i++)
-        lane_free(S->net, S->lanes[i]);
+        lane_free_n(S->nstack, S->lanes[i]);
     free(S->lanes);
     free(S);
 }
@@ -1166,7 +1203,7 @@ void orc_sessions_reset(orc_sessions *S)
 
 typedef struct {
     orc_sessions *S;
-    const int64_t *in;
+    const int64_t *in; /* NULL: resume the open calls */
     int32_t *out;
     uint8_t *status;
     uint32_t *steps;
@@ -1179,14 +1216,15 @@ static void *sworker(void *arg)
     sjob_t *j = (sjob_t *)arg;
     for (size_t i = j->lo; i < j->hi; i++) {
         uint32_t sp;
-        j->status[i] = session_call(j->S->net, j->S->lanes[i], j->in[i], j->budget, &j->out[i], &sp);
+        j->status[i] = session_step(j->S->net, j->S->lanes[i], j->in ? &j->in[i] : NULL, j->budget, &j->out[i], &sp);
         if (j->steps)
             j->steps[i] = sp;
     }
     return NULL;
 }
 
-/* One /compute call on every session i with input in[i]. */
+/* One /compute call on every session i with input in[i], or (in == NULL)
+ * one more slice of every open call. */
 int orc_sessions_compute(orc_sessions *S, const int64_t *in, int32_t *out, uint8_t *status, uint32_t *steps,
                          uint32_t budget, int threads)
 {
@@ -1213,6 +1251,14 @@ int orc_sessions_compute(orc_sessions *S, const int64_t *in, int32_t *out, uint8
     for (int t = 0; t < threads; t++)
         pthread_join(tid[t], NULL);
     return 0;
+}
+
+/* Abandon every open call (the master answered it 504): its input stays
+ * where it is if deposited, an undeposited one is dropped. */
+void orc_sessions_cancel(orc_sessions *S)
+{
+    for (size_t i = 0; i < S->n; i++)
+        S->lanes[i]->call_open = 0;
 }
 
 int orc_net_nprog(const orc_net *net) { return net->nprog; }

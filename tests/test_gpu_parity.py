@@ -543,11 +543,23 @@ def _session_pair(nodes, n, **kw):
     return g, o
 
 
-def _session_calls(nodes, seqs, **kw):
+def _session_calls(nodes, seqs, resumes=2, **kw):
+    """Every row is one call on every instance; calls left open by their
+    budget slice are resumed ``resumes`` times, then the rest are cancelled,
+    on both sides (mk_session_step(NULL) / mk_session_cancel vs the oracle's
+    session_step / orc_sessions_cancel)."""
     g, o = _session_pair(nodes, seqs.shape[1], **kw)
+    b = kw.get("budget")
     for k, row in enumerate(seqs):
         got = g.compute(row)
-        assert_same(got, o.compute(row, budget=kw.get("budget"), threads=THREADS), f"call {k}")
+        assert_same(got, o.compute(row, budget=b, threads=THREADS), f"call {k}")
+        for j in range(resumes):
+            if not ((got.status & N.MK_ST_REASON_MASK) == N.MK_ST_BUDGET).any():
+                break
+            got = g.resume()
+            assert_same(got, o.resume(budget=b, threads=THREADS), f"call {k} resume {j}")
+        g.cancel()
+        o.cancel()
     return g, o
 
 
@@ -595,9 +607,14 @@ def test_session_seq_matches_single_calls(gpu, seed):
     for k, row in enumerate(seqs):
         ref = o.compute(row, budget=budget, threads=THREADS)
         assert_same(mk.network.BatchResult(got.out[k], got.status[k], got.steps[k]), ref, f"seq call {k}")
-    # the state after the burst continues like the oracle's
+    # the state after the burst continues like the oracle's: calls still open
+    # report MK_ST_CALL_OPEN (MK_EBUSY), then resume; cancelled, a new call runs
     row = po.gen_inputs(seed + 11, 200)
-    assert_same(g.compute(row), o.compute(row, budget=budget, threads=THREADS), "after burst")
+    assert_same(g.compute(row, busy_ok=True), o.compute(row, budget=budget, threads=THREADS), "after burst")
+    assert_same(g.resume(), o.resume(budget=budget, threads=THREADS), "resumed after burst")
+    g.cancel()
+    o.cancel()
+    assert_same(g.compute(row), o.compute(row, budget=budget, threads=THREADS), "after cancel")
 
 
 def test_session_seq_single_instance_long_burst(gpu):

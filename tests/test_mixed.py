@@ -78,3 +78,80 @@ def test_gpu_node_with_remote_stack(gpu):
     finally:
         host.close()
         emu.close()
+
+
+@pytest.mark.gpu
+def test_remote_node_does_in_and_out(gpu):
+    # a reference program node r does IN / OUT against the
+    # GPU-backed master (Master.GetInput / SendOutput, master.go:233-249); g
+    # and the stack s are GPU-resident.  Checked against the oracle's session
+    # restatement of the whole network: 2x - 1 on int32 hops.
+    from misaka_net_amd.mixed import MixedHost
+
+    r_prog = "IN ACC\nMOV ACC, g:R0\nMOV R1, ACC\nOUT ACC"
+    g_prog = "MOV R0, ACC\nADD ACC\nPUSH ACC, s\nPOP s, ACC\nSUB 1\nMOV ACC, r:R1"
+    emu = refstruct.RefStructNet([("r", "program", r_prog)], start=False)
+    host = MixedHost([("g", "program", g_prog), ("s", "stack", ""), ("boss", "master", ""),
+                      ("r", "remote_program", "")], {"r": emu.addr["r"]})
+    emu.addr.update(g=host.addresses["g"])
+    emu.master_addr = host.addresses["boss"]
+    emu.start()
+    try:
+        xs = [5, -4, 2147483647, 0, -2147483648] + po.gen_inputs(0x4D49534B41, 6).tolist()
+        got = [host.compute(x, timeout=60) for x in xs]
+        ref = _oracle_calls([("g", "program", g_prog), ("r", "program", r_prog), ("s", "stack", "")], xs)
+        assert [(int(v), int(st)) for ok, v, st in got] == ref
+        assert all(ok for ok, _, _ in got)
+    finally:
+        host.close()
+        emu.close()
+
+
+@pytest.mark.gpu
+def test_timed_out_call_is_abandoned_and_calls_are_serialised(gpu):
+    # a call that times out while parked on a peer must not be
+    # resumed or overwritten by the next call, and concurrent compute() calls
+    # must not interleave their steps.  x = 0 sends to the peer r, which never
+    # reads that port, and outputs nothing: it parks until the timeout.
+    import threading
+
+    from misaka_net_amd.mixed import MixedHost
+
+    g_prog = "S: IN ACC\nJEZ Z\nOUT ACC\nJMP S\nZ: MOV ACC, r:R0\nJMP S"
+    emu = refstruct.RefStructNet([("r", "program", "MOV R1, ACC")])
+    host = MixedHost([("g", "program", g_prog), ("r", "remote_program", "")], {"r": emu.addr["r"]})
+    try:
+        ok, v, st = host.compute(0, timeout=1.0)
+        assert not ok and (st & N.MK_ST_REASON_MASK) == N.MK_ST_REMOTE_WAIT
+        assert host.compute(7, timeout=30)[:2] == (True, 7)
+        res = {}
+
+        def client(i):
+            res[i] = host.compute(100 + i, timeout=60)[:2]
+
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert res == {i: (True, 100 + i) for i in range(8)}
+    finally:
+        host.close()
+        emu.close()
+
+
+@pytest.mark.gpu
+def test_budget_resume_in_a_mixed_deployment(gpu):
+    # a long local countdown between two remote hops: the call outlives
+    # several budget slices and still answers
+    from misaka_net_amd.mixed import MixedHost
+
+    g_prog = "IN ACC\nL: SUB 1\nJGZ L\nPUSH ACC, rs\nPOP rs, ACC\nADD 9\nOUT ACC"
+    emu = refstruct.RefStructNet([("rs", "stack", "")])
+    host = MixedHost([("g", "program", g_prog), ("rs", "remote_stack", "")], {"rs": emu.addr["rs"]}, budget=1000)
+    try:
+        assert host.compute(5000, timeout=60)[:2] == (True, 9)
+        assert host.compute(3, timeout=60)[:2] == (True, 9)
+    finally:
+        host.close()
+        emu.close()
