@@ -28,11 +28,14 @@
 
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <cerrno>
+#include <climits>
+#include <cstdint>
 #include <fstream>
 #include <iterator>
 #include <string_view>
@@ -1913,25 +1916,41 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
 // One hiprtc compilation, run on a helper thread so that the caller can give
 // up after lim.max_compile_s: the job owns its inputs and outputs (shared),
 // so a compile the caller abandoned finishes in the background and is
-// discarded.
+// discarded (a helper child process is killed at once).
 struct HiprtcJob {
     std::string src;
     std::mutex mu;
     std::condition_variable cv;
     bool done = false, ok = false;
-    bool heavy = false; // a heavy stream module: worth the helper's compile too (hiprtc_run)
+    bool abandoned = false; // the caller gave up (under mu)
+    pid_t pid = 0;          // the helper child while it runs (under mu)
     std::string why;
     std::vector<char> code;
 };
 
-// The native tier's compiler.  In a process that imported PyTorch first,
-// PyTorch's bundled libhiprtc / libamd_comgr (the same sonames, an older
-// LLVM) are what the linked hiprtc symbols resolve to, and they generate
-// slower code (C4 D=256: 132 VGPRs and 325 us per launch against 75 and
-// 195 us).  So a module is compiled by mk_rtc (csrc/mk_rtc.cpp, built next to
-// this library) as a child process, which loads this ROCm install's
-// compiler; the in-process hiprtc is the fallback when the helper is missing
-// or MK_HIPRTC=linked.  MK_HIPRTC=<path> names another helper.
+// Compiles still running on detached threads: the library's teardown waits
+// for them (a thread inside comgr while static destructors run would crash).
+std::mutex g_rtc_mu;
+std::condition_variable g_rtc_cv;
+int g_rtc_running = 0;
+struct RtcDrain {
+    ~RtcDrain()
+    {
+        std::unique_lock<std::mutex> lk(g_rtc_mu);
+        (void)g_rtc_cv.wait_for(lk, std::chrono::seconds(120), [] { return g_rtc_running == 0; });
+    }
+} g_rtc_drain;
+
+// The native tier's compiler is this ROCm install's hiprtc, always: a cgo or
+// C caller links it, and so does this library.  But in a process that
+// imported PyTorch first, PyTorch's bundled libhiprtc / libamd_comgr (the
+// same sonames, an older LLVM) are what the linked hiprtc symbols resolve to
+// -- a different compiler, whose code differs from network to network (C4
+// D=256: 132 VGPRs against 75).  There the module is compiled by mk_rtc
+// (csrc/mk_rtc.cpp, built next to this library), a child process that loads
+// this ROCm's compiler, so every caller gets the same module.  The
+// in-process hiprtc is the fallback when the helper is missing or fails, or
+// with MK_HIPRTC=linked; MK_HIPRTC=<path> names another helper.
 std::string rtc_helper()
 {
     const char *e = std::getenv("MK_HIPRTC");
@@ -1945,52 +1964,83 @@ std::string rtc_helper()
     return access(path.c_str(), X_OK) == 0 ? path : std::string();
 }
 
-// Compile `src` with the helper process.  Returns false (why) when the helper
-// could not run; `ok` tells whether it compiled.
-bool rtc_spawn(const std::string &helper, const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+// Whether the linked hiprtc is another install's than this ROCm's (PyTorch's
+// bundled one in a process that imported it first).
+bool inproc_rtc_differs()
+{
+    Dl_info info{};
+    if (!dladdr(reinterpret_cast<void *>(&hiprtcCompileProgram), &info) || !info.dli_fname) return false;
+    return std::strncmp(info.dli_fname, "/opt/rocm", 9) != 0;
+}
+
+bool write_file(const std::string &path, const std::string &data)
+{
+    const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+    if (fd < 0) return false;
+    size_t off = 0;
+    while (off < data.size()) {
+        const ssize_t w = write(fd, data.data() + off, data.size() - off);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) break;
+        off += (size_t)w;
+    }
+    return close(fd) == 0 && off == data.size();
+}
+
+std::string read_file(const std::string &path, size_t max = SIZE_MAX)
+{
+    std::ifstream f(path, std::ios::binary);
+    std::string d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    return d.size() > max ? d.substr(0, max) : d;
+}
+
+// Compile with the helper process, its files in a private directory
+// (mkdtemp, 0700).  Returns false (nothing learned) when the helper could
+// not run; `ok` tells whether it compiled.
+bool rtc_spawn(const std::string &helper, HiprtcJob &j, bool &ok, std::string &why, std::vector<char> &code)
 {
     const char *td = std::getenv("TMPDIR");
     std::string base = std::string(td && *td ? td : "/tmp") + "/mk_rtc_XXXXXX";
     std::vector<char> tmpl(base.begin(), base.end());
     tmpl.push_back('\0');
-    const int fd = mkstemp(tmpl.data());
-    if (fd < 0) return false;
-    const std::string stem(tmpl.data()), in = stem + ".hip", out = stem + ".co", log = stem + ".log";
-    (void)close(fd);
+    if (!mkdtemp(tmpl.data())) return false;
+    const std::string dir(tmpl.data()), in = dir + "/lane.hip", out = dir + "/lane.co", log = dir + "/log";
     bool ran = false;
-    {
-        std::ofstream f(in, std::ios::binary);
-        f << src;
-    }
-    posix_spawn_file_actions_t fa;
-    posix_spawn_file_actions_init(&fa);
-    posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
-    posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
-    char *argv[] = {const_cast<char *>(helper.c_str()), const_cast<char *>(in.c_str()), const_cast<char *>(out.c_str()),
-                    nullptr};
-    pid_t pid = 0;
-    if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv, environ) == 0) {
-        int st = 0;
-        while (waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+    if (write_file(in, j.src)) {
+        posix_spawn_file_actions_t fa;
+        posix_spawn_file_actions_init(&fa);
+        posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0600);
+        posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
+        char *argv[] = {const_cast<char *>(helper.c_str()), const_cast<char *>(in.c_str()),
+                        const_cast<char *>(out.c_str()), nullptr};
+        pid_t pid = 0;
+        std::unique_lock<std::mutex> lk(j.mu);
+        if (!j.abandoned && posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv, environ) == 0) {
+            j.pid = pid;
+            lk.unlock();
+            int st = 0;
+            while (waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+            }
+            lk.lock();
+            j.pid = 0;
+            lk.unlock();
+            ran = WIFEXITED(st) && (WEXITSTATUS(st) == 0 || WEXITSTATUS(st) == 1);
+            ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
+            if (ok) {
+                const std::string c = read_file(out);
+                code.assign(c.begin(), c.end());
+                ok = !code.empty();
+                if (!ok) why = "mk_rtc wrote no code";
+            } else if (ran) {
+                why = read_file(log, 480);
+            }
         }
-        ran = WIFEXITED(st) && (WEXITSTATUS(st) == 0 || WEXITSTATUS(st) == 1);
-        ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
-        if (ok) {
-            std::ifstream f(out, std::ios::binary);
-            code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
-            ok = !code.empty();
-            if (!ok) why = "mk_rtc wrote no code";
-        } else if (ran) {
-            std::ifstream f(log);
-            std::string l((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-            why = l.substr(0, 480);
-        }
+        posix_spawn_file_actions_destroy(&fa);
     }
-    posix_spawn_file_actions_destroy(&fa);
     (void)unlink(in.c_str());
     (void)unlink(out.c_str());
     (void)unlink(log.c_str());
-    (void)unlink(stem.c_str());
+    (void)rmdir(dir.c_str());
     return ran;
 }
 
@@ -2021,68 +2071,30 @@ void rtc_inproc(const std::string &src, bool &ok, std::string &why, std::vector<
     (void)hiprtcDestroyProgram(&prog);
 }
 
-// VGPRs of the module's kernel: its code-object metadata (msgpack) holds
-// ".vgpr_count" once, followed by a positive integer.  0 when not found.
-uint32_t code_vgprs(const std::vector<char> &c)
-{
-    static const char key[] = "\xab.vgpr_count";
-    const std::string_view v(c.data(), c.size());
-    const size_t i = v.find(std::string_view(key, sizeof key - 1));
-    if (i == std::string_view::npos || i + sizeof key + 2 >= v.size()) return 0;
-    const auto *q = reinterpret_cast<const unsigned char *>(v.data() + i + sizeof key - 1);
-    if (q[0] < 0x80) return q[0];
-    if (q[0] == 0xcc) return q[1];
-    if (q[0] == 0xcd) return (uint32_t)q[1] << 8 | q[2];
-    return 0;
-}
-
-// Whether the linked hiprtc is another install's than the helper's (PyTorch's
-// bundled one in a process that imported it first).
-bool inproc_rtc_differs()
-{
-    Dl_info info{};
-    if (!dladdr(reinterpret_cast<void *>(&hiprtcCompileProgram), &info) || !info.dli_fname) return false;
-    return std::strncmp(info.dli_fname, "/opt/rocm", 9) != 0;
-}
-
 void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
 {
     bool ok = false;
     std::string why;
     std::vector<char> code;
-    // Heavy modules: the helper's module (this ROCm's compiler); where the
-    // in-process compiler is another one, its module too, and the one whose
-    // kernel needs fewer VGPRs is kept -- each compiler wins some networks (C4
-    // D=64: 58 vs 94 VGPRs, 59 vs 72 us, for the in-process one; D=256: 75
-    // vs 132 VGPRs, 191 vs 319 us, for the helper's).
-    // Only heavy stream modules, where the two compilers' register use
-    // differs most, pay for a second compile and a helper process (≈0.3 s to
-    // start); the others compile in process.
-    const std::string helper = j->heavy ? rtc_helper() : std::string();
-    const bool spawned = !helper.empty() && rtc_spawn(helper, j->src, ok, why, code);
-    std::string from = spawned ? "helper" : "inproc";
-    if (!spawned || inproc_rtc_differs()) {
-        bool ok2 = false;
-        std::string why2;
-        std::vector<char> code2;
-        rtc_inproc(j->src, ok2, why2, code2);
-        const uint32_t v1 = ok ? code_vgprs(code) : 0u, v2 = ok2 ? code_vgprs(code2) : 0u;
-        if (ok2 && (!ok || (v2 && v1 && v2 < v1))) {
-            ok = true;
-            code = std::move(code2);
-            why.clear();
-            from = "inproc";
-        } else if (!ok) {
-            why = why2;
-        }
+    const std::string helper = inproc_rtc_differs() ? rtc_helper() : std::string();
+    const bool spawned = !helper.empty() && rtc_spawn(helper, *j, ok, why, code);
+    std::string from = "helper";
+    if (!spawned) {
+        rtc_inproc(j->src, ok, why, code);
+        from = inproc_rtc_differs() ? "linked-other" : "linked";
     }
     if (ok) why = from; // which compiler's module (mk_net_plan)
-    std::lock_guard<std::mutex> lk(j->mu);
-    j->ok = ok;
-    j->why = std::move(why);
-    j->code = std::move(code);
-    j->done = true;
-    j->cv.notify_all();
+    {
+        std::lock_guard<std::mutex> lk(j->mu);
+        j->ok = ok;
+        j->why = std::move(why);
+        j->code = std::move(code);
+        j->done = true;
+        j->cv.notify_all();
+    }
+    std::lock_guard<std::mutex> lk(g_rtc_mu);
+    --g_rtc_running;
+    g_rtc_cv.notify_all();
 }
 
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
@@ -2114,13 +2126,18 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
-    job->heavy = J.heavy;
     J.src_bytes = job->src.size();
+    {
+        std::lock_guard<std::mutex> lk(g_rtc_mu);
+        ++g_rtc_running;
+    }
     std::thread(hiprtc_run, job).detach();
     {
         std::unique_lock<std::mutex> lk(job->mu);
         const auto limit = std::chrono::duration<double>(lim.max_compile_s);
         if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+            job->abandoned = true; // a helper child is killed; an in-process compile runs out
+            if (job->pid > 0) (void)kill(job->pid, SIGKILL);
             char b[128];
             snprintf(b, sizeof b, "hiprtc did not finish within the native tier's compile bound (%.0f s)",
                      lim.max_compile_s);

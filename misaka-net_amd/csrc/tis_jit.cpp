@@ -82,6 +82,7 @@ struct Graph {
     std::vector<uint32_t> entry;
     std::vector<char> seen;      // variant reachable from variant 0
     std::vector<char> used_reg;  // register read or written by reachable code
+    std::vector<char> narrow;    // register whose high 32 bits nothing reads (narrow_regs): uint32_t
     size_t nreach = 0, ndops = 0; // ndops: micro-ops emitted (rolled runs count once)
     bool cyclic = false;
     std::vector<std::vector<Run>> runs; // per variant, ascending start
@@ -317,6 +318,62 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
         }
     }
     return true;
+}
+
+// Registers whose high 32 bits no reachable op ever reads.  ACC and BAK are
+// int64 (program.go:27-28) and every hop truncates to int32 (program.go:498,
+// 516, 561), so a register that only ever feeds hops -- stack slots, the
+// /compute output, port hand-offs to sext32 uses -- or other such registers
+// through ADD/SUB/MOV (whose low 32 bits depend on their operands' low 32
+// bits only) can be computed in 32 bits with identical results.  The high
+// bits are read by BR/BRX conditions and JRO operands without UF_TA (the
+// full int64 ACC decides, program.go:315-363), by dynamic-stack depth
+// operands (STX/LDX/OVF b), and by any op writing a register that needs
+// them.  A backward fixpoint over the reachable ops, flow-insensitive.
+// C4's pipeline then runs its `sum = 3 * sum + v` chains as 32-bit adds
+// instead of 64-bit ones (half the VALU work, and the same code from either
+// hiprtc).  Stream shape only: the machine shape's loop phases keep int64.
+void narrow_regs(Graph &g)
+{
+    const size_t R = g.used_reg.size();
+    std::vector<char> wide(R, 0);
+    std::vector<const DOp *> ops;
+    for (uint32_t v = 0; v < g.entry.size(); ++v) {
+        if (!g.seen[v]) continue;
+        for (size_t pc = g.entry[v];; ++pc) {
+            const DOp &I = g.D[pc];
+            ops.push_back(&I);
+            if (I.op == U_JUMP || I.op == U_BR || I.op == U_JRO || I.op == U_END) break;
+        }
+    }
+    auto mark = [&](uint32_t off) {
+        const uint32_t r = off / 8;
+        if (r < R && !wide[r]) { wide[r] = 1; return true; }
+        return false;
+    };
+    for (const DOp *I : ops) {
+        switch (I->op) {
+        case U_BR: case U_BRX: case U_JRO: if (!(I->fl & UF_TA)) mark(I->a); break;
+        case U_STX: case U_LDX: case U_OVF: mark(I->b); break;
+        default: break;
+        }
+    }
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (const DOp *I : ops) {
+            if (!(I->d / 8 < R && wide[I->d / 8])) continue;
+            switch (I->op) {
+            case U_MOV: case U_ADDI: case U_RSUBI: if (!(I->fl & UF_TA)) changed |= mark(I->a); break;
+            case U_ADD: case U_SUB:
+                if (!(I->fl & UF_TA)) changed |= mark(I->a);
+                if (!(I->fl & UF_TB)) changed |= mark(I->b);
+                break;
+            default: break;
+            }
+        }
+    }
+    g.narrow.assign(R, 0);
+    for (size_t r = 0; r < R; ++r) g.narrow[r] = g.used_reg[r] && !wide[r];
 }
 
 // Micro-op emission shared by both shapes.  `R` prefixes register names
@@ -814,7 +871,7 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
     e.line("{");
     for (uint32_t r = 0; r < p.nregs; ++r)
-        if (g.used_reg[r]) e.line("    int64_t r%u = 0;", r);
+        if (g.used_reg[r]) e.line("    %s r%u = 0;", r < g.narrow.size() && g.narrow[r] ? "uint32_t" : "int64_t", r);
     e.line("    r%u = (int64_t)(int32_t)in;", p.in_reg);
     e.line("    uint32_t steps = 0, st = 0;");
     e.line("    int32_t outv = 0;");
@@ -1562,10 +1619,12 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
         }
         *pool = m;
     }
-    if (s == JIT_MACHINE)
+    if (s == JIT_MACHINE) {
         emit_machine_lane(p, g, e);
-    else
+    } else {
+        if (lim.narrow) narrow_regs(g);
         emit_stream(p, g, e, max_fast_steps(p, g), checked);
+    }
     if (!checked && e.s.size() > lim.max_src_bytes) {
         why = "lane source of " + std::to_string(e.s.size()) + " B exceeds the native tier's compile bound (" +
               std::to_string(lim.max_src_bytes) + " B)";
@@ -1985,6 +2044,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
     flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
+    flag("MK_JIT_NARROW", l.narrow);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -1994,12 +2054,12 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)ts_dyn,
              (int)tune_regs,
-             lds_split, (int)lds_volatile);
+             lds_split, (int)lds_volatile, (int)narrow);
     return b;
 }
 

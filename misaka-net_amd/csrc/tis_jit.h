@@ -106,6 +106,9 @@ struct JitLimits {
     // lanes without stack slots, 4 with them -- r02ak: C5 212-214 vs 215 us
     // but the JRO-heavy census class 58.9 vs 52.1 ms, so not the default.
     uint32_t ts_rounds = 4;
+    // Stream shape: registers whose high 32 bits nothing reads are computed
+    // in 32 bits (narrow_regs in tis_jit.cpp; MK_JIT_NARROW=0: all int64).
+    bool narrow = true;
     // Its chunks: taken by whichever wave of the block is free, highest
     // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
     // order.
