@@ -56,9 +56,12 @@ struct Ctl {
     std::vector<uint32_t> depth; // entries tracked symbolically (dynamic stacks: above the memory part)
     std::vector<uint8_t> lo;     // dynamic stacks: known lower bound of the memory depth (0 or 1)
     bool in_avail = true;
-    uint8_t out_cnt = 0;
+    uint8_t out_cnt = 0; // sessions: outChan full (0/1)
     uint8_t pos = 0;
     bool changed = false;
+    // sessions: the call's input is deposited into inChan; the call's
+    // round-start checks (deposit, take) are still to run at this state
+    bool cdep = false, pre = false;
 };
 
 struct StackDigest {
@@ -85,10 +88,11 @@ enum { A_CONT = 0, A_EXIT = 1 };
 
 class Compiler {
   public:
-    Compiler(const Network &net, uint32_t cap, bool soo, const SchedLimits &lim, const std::vector<uint8_t> &dyn)
-        : net_(net), cap_(cap), soo_(soo), lim_(lim), N_(net.nprog), S_(net.uses_stacks ? net.nstack : 0)
+    Compiler(const Network &net, uint32_t cap, bool soo, const SchedLimits &lim, const std::vector<uint8_t> &dyn,
+             bool sess = false)
+        : net_(net), cap_(cap), soo_(soo), sess_(sess), lim_(lim), N_(net.nprog), S_(net.uses_stacks ? net.nstack : 0)
     {
-        L0_ = 7 * N_ + 2 + S_;
+        L0_ = 7 * N_ + 2 + S_ + (sess ? 1 : 0);
         home_.assign(L0_, -1);
         dyn_base_.assign(S_, -1);
         for (int s = 0; s < S_; s++)
@@ -110,11 +114,13 @@ class Compiler {
     int INL() const { return 7 * N_; }
     int OUTL() const { return 7 * N_ + 1; }
     int DEP(int s) const { return 7 * N_ + 2 + s; } // dynamic stack: entries in memory
-    bool is32(int loc) const { return loc >= 2 * N_ && loc < 7 * N_ + 2; }
+    int CIN() const { return 7 * N_ + 2 + S_; }     // sessions: the call's input, not yet deposited
+    bool is32(int loc) const { return (loc >= 2 * N_ && loc < 7 * N_ + 2) || (sess_ && loc == CIN()); }
 
     const Network &net_;
     uint32_t cap_;
     bool soo_;
+    bool sess_; // stateful sessions: calls, inChan / outChan as channels (session_step)
     SchedLimits lim_;
     int N_, S_, L0_;
     std::vector<std::vector<uint8_t>> acc_live_, bak_live_;
@@ -395,6 +401,11 @@ class Compiler {
     bool inline_pop_check(int s);
     void round_end_marker();
     void generalize();
+    // sessions
+    void exit_yield(uint8_t reason);
+    bool session_round_start();
+    uint8_t out_bit() const { return !sess_ && ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0; }
+    Val out_val() const { return sess_ ? vconst(0) : loc_[OUTL()]; }
 
     int attempt(int n);
     void compile_entry(uint32_t id);
@@ -471,6 +482,10 @@ void Compiler::prune(Ctl &c, std::vector<Val> &loc) const
     for (int s = 0; s < 4 * N_; s++)
         if (!((c.pfull >> s) & 1ull)) loc[PORT(s)] = vdead();
     if (!c.in_avail) loc[INL()] = vdead();
+    if (sess_) {
+        if (!c.out_cnt) loc[OUTL()] = vdead();
+        if (c.cdep) loc[CIN()] = vdead();
+    }
 }
 
 // key_of without the constants' values (what widening compares)
@@ -493,8 +508,9 @@ std::string Compiler::key_of(const Ctl &c, const std::vector<Val> &loc, const st
     put(&c.pfull, 8);
     put(c.depth.data(), c.depth.size() * 4);
     put(c.lo.data(), c.lo.size());
-    const uint8_t misc[4] = {(uint8_t)c.in_avail, c.out_cnt, c.pos, (uint8_t)c.changed};
-    put(misc, 4);
+    const uint8_t misc[6] = {(uint8_t)c.in_avail, c.out_cnt, c.pos, (uint8_t)c.changed, (uint8_t)c.cdep,
+                             (uint8_t)c.pre};
+    put(misc, 6);
     for (int X = 0; X < L0_; X++) {
         const Val &v = loc[X];
         const uint8_t kd = v.kind == K_MEM ? K_REG : v.kind;
@@ -749,8 +765,8 @@ void Compiler::exit_jump()
 
 void Compiler::exit_end(uint8_t reason)
 {
-    const Val &o = loc_[OUTL()];
-    const uint8_t st = reason | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+    const Val o = out_val();
+    const uint8_t st = reason | out_bit();
     if (o.kind == K_REG) emit(U_END, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, 0, 0);
     else emit(U_END, 0, st, 0, 0, o.kind == K_CONST ? o.c : 0);
     emit_ext(steps_);
@@ -867,11 +883,66 @@ void Compiler::exit_pop_check(int s)
 
 void Compiler::round_end_marker()
 {
-    const Val &o = loc_[OUTL()];
-    const uint8_t st = MK_ST_BUDGET | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+    const Val o = out_val();
+    const uint8_t st = MK_ST_BUDGET | out_bit();
     if (o.kind == K_REG) emit(U_ROUND_END, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, 0, 0);
     else emit(U_ROUND_END, 0, st, 0, 0, o.kind == K_CONST ? o.c : 0);
     emit_ext(steps_);
+}
+
+// Sessions: a /compute call ends -- its output taken from outChan
+// (MK_ST_HAS_OUTPUT) or a round without change (MK_ST_QUIESCENT: nothing can
+// change without another input; the instance keeps its state).  The next
+// call starts at the successor state with its input in CIN's home.
+void Compiler::exit_yield(uint8_t reason)
+{
+    Ctl c = ctl_;
+    c.pre = true;
+    c.cdep = false;
+    c.pos = 0;
+    c.changed = false;
+    Val o;
+    if (reason & MK_ST_HAS_OUTPUT) {
+        o = loc_[OUTL()];
+        c.out_cnt = 0;
+    }
+    // the next call's input arrives in CIN's home (nothing else ever lives
+    // there, so nothing moves), and the successor's shape must say so for
+    // widening to see repeated states (a running sum across calls)
+    Val in;
+    in.kind = K_REG;
+    in.r = (uint16_t)home_[CIN()];
+    set_loc(CIN(), in);
+    std::vector<Ctl> succ{c};
+    std::vector<std::vector<Val>> sl;
+    o = canonicalize(succ, sl, o);
+    if (fail_) return;
+    const uint32_t id = get_or_create(succ[0], sl[0]);
+    if (fail_) return;
+    const int64_t oc = o.kind == K_CONST ? sext32(o.c) : 0;
+    if (o.kind == K_REG) emit(U_YIELD, (uint8_t)(UF_OUTREG | fa(o)), reason, o.r, 0, 2 * (int64_t)id);
+    else emit(U_YIELD, 0, reason, 0, 0, 2 * (int64_t)id);
+    emit_ext((int64_t)(((uint64_t)(uint32_t)oc << 32) | steps_));
+}
+
+// Sessions: the checks at the top of every round (tis_oracle.c
+// session_step): the call's input goes into inChan once it is empty
+// (m.inChan <- v, master.go:216); once deposited, a value in outChan ends
+// the call (<-m.outChan, :219).  Returns true when the call ended.
+bool Compiler::session_round_start()
+{
+    ctl_.pre = false;
+    if (!ctl_.cdep && !ctl_.in_avail) {
+        ctl_.in_avail = true;
+        set_loc(INL(), loc_[CIN()]);
+        set_loc(CIN(), vdead());
+        ctl_.cdep = true;
+    }
+    if (ctl_.cdep && ctl_.out_cnt) {
+        exit_yield(MK_ST_HAS_OUTPUT);
+        return true;
+    }
+    return false;
 }
 
 void Compiler::generalize()
@@ -1058,6 +1129,20 @@ int Compiler::attempt(int n)
         break;
     }
     case OP_OUT:
+        if (sess_) { // outChan <- v blocks while full (master.go:246, capacity 1 :59)
+            if (!ctl_.out_cnt) {
+                set_loc(OUTL(), trunc(v));
+                ctl_.out_cnt = 1;
+                ctl_.pend &= ~(1u << n);
+                set_loc(PENDV(n), vdead());
+                retire();
+            } else if (!pn) {
+                ctl_.pend |= 1u << n;
+                set_loc(PENDV(n), trunc(v));
+                ctl_.changed = true;
+            }
+            break;
+        }
         if (ctl_.out_cnt < 2) {
             if (ctl_.out_cnt == 0) set_loc(OUTL(), trunc(v));
             ctl_.out_cnt++;
@@ -1084,8 +1169,8 @@ int Compiler::attempt(int n)
             break;
         }
         if (D.kind == K_REG) { // the lane overflows here iff DEP >= cap - depth
-            const Val &o = loc_[OUTL()];
-            const uint8_t st = MK_ST_STACK_OVERFLOW | (ctl_.out_cnt > 0 ? MK_ST_HAS_OUTPUT : 0);
+            const Val o = out_val();
+            const uint8_t st = MK_ST_STACK_OVERFLOW | out_bit();
             const uint64_t lim = cap_ - ctl_.depth[s];
             if (o.kind == K_REG) emit(U_OVF, (uint8_t)(UF_OUTREG | fa(o)), st, o.r, D.r, 0);
             else emit(U_OVF, 0, st, 0, D.r, o.kind == K_CONST ? o.c : 0);
@@ -1118,14 +1203,23 @@ void Compiler::compile_entry(uint32_t id)
     std::unordered_set<std::string> seen;
     size_t last_size = 0;
     uint32_t idle = 0;
-    for (;;) {
+    bool done = sess_ && ctl_.pre && session_round_start(); // a call's first round start
+    for (; !done;) {
         if (fail_) return;
         if (ctl_.pos == N_) {
             if (!ctl_.changed) {
-                exit_end(MK_ST_QUIESCENT);
+                if (sess_) exit_yield(MK_ST_QUIESCENT); // the call closes; the instance lives on
+                else exit_end(MK_ST_QUIESCENT);
                 break;
             }
-            round_end_marker();
+            if (sess_) { // session_step: deposit, take, then the budget check
+                ctl_.pos = 0;
+                ctl_.changed = false;
+                if (session_round_start()) break;
+                round_end_marker();
+            } else {
+                round_end_marker();
+            }
             ctl_.pos = 0;
             ctl_.changed = false;
             if (++rounds_ > lim_.max_rounds) { failf("symbolic round budget exceeded"); return; }
@@ -1184,7 +1278,8 @@ void Compiler::share_slots()
     if (!lim_.share_slots || !any_slot_ || max_slot_ < 2) return;
     const size_t nsb = sb_code_.size();
     auto two_words = [](uint8_t op) {
-        return op == U_BR || op == U_JRO || op == U_END || op == U_ROUND_END || op == U_OVF || op == U_BRX;
+        return op == U_BR || op == U_JRO || op == U_END || op == U_ROUND_END || op == U_OVF || op == U_BRX ||
+               op == U_YIELD;
     };
     // superblock successors (exits and side exits)
     std::vector<std::vector<uint32_t>> succ(nsb);
@@ -1192,7 +1287,8 @@ void Compiler::share_slots()
         const std::vector<UOp> &sc = sb_code_[id];
         for (size_t i = 0; i < sc.size(); i++) {
             const UOp &u = sc[i];
-            if (u.op == U_JUMP || u.op == U_BRX) succ[id].push_back((uint32_t)(u.imm / 2));
+            // a session's next call goes on with the state a yield leaves
+            if (u.op == U_JUMP || u.op == U_BRX || u.op == U_YIELD) succ[id].push_back((uint32_t)(u.imm / 2));
             else if (u.op == U_BR) {
                 succ[id].push_back((uint32_t)((uint64_t)u.imm & 0xFFFFFFFFu) / 2);
                 succ[id].push_back((uint32_t)((uint64_t)u.imm >> 32) / 2);
@@ -1342,6 +1438,10 @@ bool Compiler::run(SchedProgram &out, std::string &why)
     c.ip.assign(N_, 0);
     c.depth.assign(S_, 0);
     c.lo.assign(S_, 0);
+    if (sess_) { // a session at the start of its first call: inChan and outChan empty
+        c.in_avail = false;
+        c.pre = true;
+    }
     ctl_ = c;
     loc_.assign(L0_, vdead());
     for (int s = 0; s < S_; s++) loc_[DEP(s)] = vconst(0);
@@ -1349,16 +1449,17 @@ bool Compiler::run(SchedProgram &out, std::string &why)
         loc_[ACC(n)] = vconst(0);
         loc_[BAK(n)] = vconst(0);
     }
-    loc_[OUTL()] = vconst(0);
+    if (!sess_) loc_[OUTL()] = vconst(0);
     stk_.assign(S_, {});
     dig_.assign(S_, StackDigest());
     ensure_reg(0);
-    home_[INL()] = 0;
+    const int inloc = sess_ ? CIN() : INL(); // the input's location: a call's input / inChan
+    home_[inloc] = 0;
     claimed_[0] = 1;
     Val in;
     in.kind = K_REG;
     in.r = 0;
-    loc_[INL()] = in;
+    loc_[inloc] = in;
     prune(ctl_, loc_);
     get_or_create(ctl_, loc_);
     while (!work_.empty() && !fail_) {
@@ -1383,7 +1484,7 @@ bool Compiler::run(SchedProgram &out, std::string &why)
                 maxinc = std::max<int64_t>(maxinc, sc[i + 1].imm);
                 i++;
             } else if (sc[i].op == U_BR || sc[i].op == U_JRO || sc[i].op == U_END || sc[i].op == U_OVF ||
-                       sc[i].op == U_BRX) {
+                       sc[i].op == U_BRX || sc[i].op == U_YIELD) {
                 i++;
             }
         }
@@ -1400,7 +1501,13 @@ bool Compiler::run(SchedProgram &out, std::string &why)
             if (sc[i].op == U_ROUND_END) { i++; continue; }
             out.code.push_back(sc[i]);
         }
-        if (maxinc >= 0) {
+        if (maxinc >= 0 && sess_) { // sessions: the interpreter runs the rest of the call
+            out.entry[2 * id + 1] = (uint32_t)out.code.size();
+            UOp h{};
+            h.op = U_HANDOFF;
+            h.imm = 2 * (int64_t)id;
+            out.code.push_back(h);
+        } else if (maxinc >= 0) {
             out.entry[2 * id + 1] = (uint32_t)out.code.size();
             out.code.insert(out.code.end(), sc.begin(), sc.end());
         } else {
@@ -1414,6 +1521,43 @@ bool Compiler::run(SchedProgram &out, std::string &why)
     out.in_reg = 0;
     out.nsb = (uint32_t)entries_.size();
     out.sym_rounds = rounds_;
+    if (sess_) {
+        out.session = true;
+        out.nloc = (uint32_t)L0_;
+        out.dyn_base = dyn_base_;
+        out.smap.resize(entries_.size());
+        for (size_t id = 0; id < entries_.size(); id++) {
+            const EntryState &e = entries_[id];
+            SessEntry &m = out.smap[id];
+            m.ip = e.ctl.ip;
+            m.pend = e.ctl.pend;
+            m.hung = e.ctl.hung;
+            m.pfull = e.ctl.pfull;
+            m.in_avail = e.ctl.in_avail;
+            m.out_full = e.ctl.out_cnt != 0;
+            m.deposited = e.ctl.cdep;
+            m.pos = e.ctl.pos;
+            m.changed = e.ctl.changed;
+            m.pre = e.ctl.pre;
+            m.loc.resize(L0_);
+            for (int X = 0; X < L0_; X++) {
+                const Val &v = e.loc[X];
+                if (v.kind == K_CONST) m.loc[X].kind = 1, m.loc[X].c = v.c;
+                else if (v.kind == K_REG) m.loc[X].kind = 2, m.loc[X].r = v.r;
+            }
+            m.stk.resize(S_);
+            for (int s = 0; s < S_; s++) {
+                if (dyn(s)) continue;
+                for (uint32_t d = 0; d < (uint32_t)e.stk[s].size(); d++) {
+                    const Val &v = e.stk[s][d];
+                    SessSrc x;
+                    if (v.kind == K_CONST) x.kind = 1, x.c = v.c;
+                    else x.kind = 3, x.r = ndyn_ * cap_ + (uint32_t)slot_id_[s][d];
+                    m.stk[s].push_back(x);
+                }
+            }
+        }
+    }
     return true;
 }
 
@@ -1437,8 +1581,9 @@ SchedLimits lim_env(SchedLimits lim)
     return lim;
 }
 
-bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
-                      SchedProgram &out, std::string &why)
+namespace {
+bool compile_any(const Network &net, uint32_t stack_cap, bool stop_on_output, bool sess, const SchedLimits &lim,
+                 SchedProgram &out, std::string &why)
 {
     if (net.uses_remote) { // X-ops wait on the host: only the interpreters run them
         why = "network addresses remote peers (MK_NODE_REMOTE_*)";
@@ -1450,13 +1595,26 @@ bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_outpu
     std::vector<uint8_t> dyn(S, 0);
     const SchedLimits L = lim_env(lim);
     for (;;) {
-        Compiler c(net, stack_cap, stop_on_output, L, dyn);
+        Compiler c(net, stack_cap, stop_on_output, L, dyn, sess);
         if (c.run(out, why)) return true;
         bool more = false;
         for (int s = 0; s < S; s++)
             if (c.want_dyn()[s] && !dyn[s]) dyn[s] = 1, more = true;
         if (!more) return false;
     }
+}
+} // namespace
+
+bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
+                      SchedProgram &out, std::string &why)
+{
+    return compile_any(net, stack_cap, stop_on_output, false, lim, out, why);
+}
+
+bool compile_session_schedule(const Network &net, uint32_t stack_cap, const SchedLimits &lim, SchedProgram &out,
+                              std::string &why)
+{
+    return compile_any(net, stack_cap, false, true, lim, out, why);
 }
 
 std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std::vector<uint32_t> &entry_out)
@@ -1472,7 +1630,7 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
         o.fl = u.fl;
         o.imm = u.imm;
         const bool two = u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF ||
-                         u.op == U_BRX;
+                         u.op == U_BRX || u.op == U_YIELD;
         const uint32_t ext = two ? (uint32_t)p.code[i + 1].imm : 0;
         switch (u.op) {
         case U_MOV: case U_ADDI: case U_RSUBI:
@@ -1497,6 +1655,14 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
             o.a = u.a * scale; o.b = u.b * scale; break;
         case U_LDX:
             o.d = u.d * scale; o.b = u.b * scale; break;
+        case U_YIELD: { // imm = next variant | out constant << 32, inc = steps
+            const uint64_t x = (uint64_t)p.code[i + 1].imm;
+            o.d = u.d;
+            o.a = (u.fl & UF_OUTREG) ? u.a * scale : 0;
+            o.inc = (uint32_t)x;
+            o.imm = (int64_t)(((x >> 32) << 32) | (uint32_t)u.imm);
+            break;
+        }
         case U_OVF: {
             const uint64_t x = (uint64_t)p.code[i + 1].imm;
             o.d = u.d;
@@ -1517,11 +1683,36 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
     return out;
 }
 
+void build_sess_map(const SchedProgram &p, int nprog, int nstack, std::vector<SessMapHdr> &hdr,
+                    std::vector<SessSrcDev> &rec)
+{
+    hdr.clear();
+    rec.clear();
+    auto put = [&](const SessSrc &x) { rec.push_back(SessSrcDev{x.c, x.r, x.kind}); };
+    for (const SessEntry &m : p.smap) {
+        SessMapHdr h{};
+        h.off = (uint32_t)rec.size();
+        h.pend = m.pend;
+        h.hung = m.hung;
+        h.pfull = m.pfull;
+        h.flags = (m.in_avail ? 1u : 0u) | (m.out_full ? 2u : 0u) | (m.deposited ? 4u : 0u) | (m.changed ? 8u : 0u) |
+                  (m.pre ? 16u : 0u) | (uint32_t)m.pos << 8;
+        hdr.push_back(h);
+        for (int n = 0; n < nprog; n++) rec.push_back(SessSrcDev{(int64_t)m.ip[n], 0u, 1u});
+        for (const SessSrc &x : m.loc) put(x);
+        for (int s = 0; s < nstack; s++) {
+            const size_t k = (size_t)s < m.stk.size() ? m.stk[s].size() : 0;
+            rec.push_back(SessSrcDev{(int64_t)k, 0u, 1u});
+            for (size_t d = 0; d < k; d++) put(m.stk[s][d]);
+        }
+    }
+}
+
 std::string sched_disasm(const SchedProgram &p)
 {
     static const char *names[U_COUNT] = {"MOV", "LI",  "ADD", "SUB", "ADDI",  "RSUBI",     "ST",  "STI", "LD",
                                          "STX", "LDX", "JUMP", "BR", "JRO", "END", "GUARD", "ROUND_END", "OVF",
-                                         "BRX"};
+                                         "BRX", "YIELD", "HANDOFF"};
     std::string s;
     char buf[200];
     snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu\n", p.nsb, p.nregs, p.nslots,
@@ -1540,7 +1731,8 @@ std::string sched_disasm(const SchedProgram &p)
         snprintf(buf, sizeof buf, "  %5zu %-9s fl=%02x d=%u a=%u b=%u imm=%lld\n", i, nm, u.fl, u.d, u.a, u.b,
                  (long long)u.imm);
         s += buf;
-        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF || u.op == U_BRX) {
+        if (u.op == U_BR || u.op == U_JRO || u.op == U_END || u.op == U_ROUND_END || u.op == U_OVF || u.op == U_BRX ||
+            u.op == U_YIELD) {
             i++;
             snprintf(buf, sizeof buf, "        ext       steps+=%lld\n", (long long)p.code[i].imm);
             s += buf;

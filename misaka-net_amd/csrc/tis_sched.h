@@ -40,6 +40,12 @@ enum UOpCode : uint8_t {
     U_OVF,      // if R[b] >= hi32(ext.imm): steps += lo32(ext.imm); END(status d, out A|imm)
                 // (a PUSH onto a dynamic stack at its capacity)                 (2 words)
     U_BRX,      // if cond(A): steps += ext.imm; sb = imm (an in-line side exit)  (2 words)
+    // sessions (compile_session_schedule) only:
+    U_YIELD,    // a /compute call ends: steps += lo32(ext.imm); out = OUTREG ? A : hi32(ext.imm);
+                // status = d; the session's next call starts at variant imm        (2 words)
+    U_HANDOFF,  // the budget slice ends inside this superblock: the lane leaves at the
+                // entry of variant imm (its state: SchedProgram::smap) for the
+                // bytecode interpreter, which runs the rest of the call      (1 word)
     U_COUNT
 };
 
@@ -76,6 +82,52 @@ struct SchedLimits {
     bool share_slots = true;               // acyclic graphs: stacks never in use together share slots
 };
 
+// Stateful sessions (row f2): the state at a superblock entry, as the
+// bytecode interpreter's session state needs it (a lane handed off there,
+// U_HANDOFF).  Locations are those of the compiler (tis_sched.cpp): ACC(n),
+// BAK(n), PORT(4n+k), PENDV(n), INL, OUTL, DEP(s), CIN; each is dead, a
+// constant, or in register r.  Stack entries are constants or in slot r.
+struct SessSrc {
+    uint8_t kind = 0; // 0 dead, 1 constant c, 2 register r, 3 slot r
+    uint32_t r = 0;
+    int64_t c = 0;
+};
+struct SessEntry {
+    std::vector<uint16_t> ip;
+    uint32_t pend = 0, hung = 0;
+    uint64_t pfull = 0;
+    bool in_avail = false, out_full = false, deposited = false;
+    uint8_t pos = 0;      // the next program node to attempt in the current round
+    bool changed = false; // something changed earlier in that round
+    bool pre = false;     // the call's round-start checks are still to run
+    std::vector<SessSrc> loc;              // every location, in the compiler's order
+    std::vector<std::vector<SessSrc>> stk; // ordinary stacks: their entries, bottom first
+};
+
+// Device form of the session state map (SchedProgram::smap), one header per
+// superblock and 16-byte records: at `off`, the nprog instruction pointers
+// (constants), then every location in the compiler's order (ACC(n), BAK(n),
+// PORT(q), PENDV(n), INL, OUTL, DEP(s), CIN), then per stack a count (a
+// constant; 0 for dynamic stacks, whose entries are slots base + j below
+// DEP) followed by that many entries.  Read by sess_convert.h.
+struct SessSrcDev {
+    int64_t c;     // constant
+    uint32_t r;    // register or slot
+    uint32_t kind; // SessSrc::kind
+};
+static_assert(sizeof(SessSrcDev) == 16, "SessSrcDev must be 16 bytes");
+struct SessMapHdr {
+    uint32_t off;   // first record
+    uint32_t pend, hung;
+    uint32_t flags; // in_avail | out_full << 1 | deposited << 2 | changed << 3 | pre << 4 | pos << 8
+    uint64_t pfull;
+};
+static_assert(sizeof(SessMapHdr) == 24, "SessMapHdr must be 24 bytes");
+
+struct SchedProgram;
+void build_sess_map(const SchedProgram &p, int nprog, int nstack, std::vector<SessMapHdr> &hdr,
+                    std::vector<SessSrcDev> &rec);
+
 struct SchedProgram {
     std::vector<UOp> code;
     std::vector<uint32_t> entry; // variant id -> first word; 2k = fast, 2k+1 = budget-checked
@@ -86,6 +138,12 @@ struct SchedProgram {
     uint32_t in_reg = 0;         // register holding the lane input at entry
     uint32_t nsb = 0;            // superblocks
     uint64_t sym_rounds = 0;     // rounds executed symbolically
+    // sessions: every superblock's entry state (U_HANDOFF), the dynamic
+    // stacks' first slots (-1: ordinary), the location count
+    bool session = false;
+    std::vector<SessEntry> smap;
+    std::vector<int64_t> dyn_base;
+    uint32_t nloc = 0;
 };
 
 // Device form of a micro-op (32 bytes = one s_load_dwordx8): every field is
@@ -119,6 +177,16 @@ std::vector<DOp> assemble_device(const SchedProgram &p, uint32_t reg_bytes, std:
 // the caller then uses the direct bytecode interpreter.
 bool compile_schedule(const Network &net, uint32_t stack_cap, bool stop_on_output, const SchedLimits &lim,
                       SchedProgram &out, std::string &why);
+
+// The same network compiled for stateful sessions (SURVEY.md section 8 row
+// f2; oracle session_step): variant 0 is the post-/reset instance at the
+// start of a /compute call whose input is in register in_reg.  A call ends
+// in U_YIELD (its output taken, or a round without change: the next call
+// starts at the yield's variant, again with its input in in_reg) or U_END
+// (a stack overflow ends the session).  Budget-checked variants are a
+// U_HANDOFF each: the rest of such a call runs on the interpreter.
+bool compile_session_schedule(const Network &net, uint32_t stack_cap, const SchedLimits &lim, SchedProgram &out,
+                              std::string &why);
 
 std::string sched_disasm(const SchedProgram &p);
 

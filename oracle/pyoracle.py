@@ -26,8 +26,11 @@ def build(force: bool = False) -> str:
     """Compile the oracle with gcc (no GPU needed)."""
     import hashlib
 
-    with open(SRC, "rb") as f:
-        stamp = hashlib.sha256(f.read()).hexdigest()  # content, not mtime: the tree travels to the GPU box
+    h = hashlib.sha256()
+    for src in (SRC, os.path.join(os.path.dirname(SRC), "orc_flat.h")):
+        with open(src, "rb") as f:
+            h.update(f.read())
+    stamp = h.hexdigest()  # content, not mtime: the tree travels to the GPU box
     try:
         with open(LIB + ".stamp") as f:
             fresh = os.path.exists(LIB) and f.read().strip() == stamp
@@ -82,6 +85,7 @@ def lib():
         h.orc_sessions_free.argtypes = [C.c_void_p]
         h.orc_sessions_reset.argtypes = [C.c_void_p]
         h.orc_sessions_cancel.argtypes = [C.c_void_p]
+        h.orc_session_import.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         h.orc_sessions_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                            C.c_int]
         h.orc_go_atoi.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64)]
@@ -227,6 +231,12 @@ class OracleSessions:
     def cancel(self):
         """Abandon every open call (the master answered it 504)."""
         lib().orc_sessions_cancel(self._h)
+
+    def import_state(self, i, flat):
+        """Instance i takes a handed-off state (orc_flat.h: a ctypes
+        structure, its entries buffer kept alive by the caller) with its
+        call open; the next resume() finishes that call."""
+        assert lib().orc_session_import(self._h, i, C.addressof(flat)) == 0
 
 
 def gen_inputs(seed: int, n: int, *, kind: int = 0, mask: int = 0, offset: int = 0) -> np.ndarray:

@@ -39,6 +39,7 @@
 #include <string.h>
 
 #define ORC_MAX_NODES 64
+#include "orc_flat.h"
 
 /* status byte layout (shared with include/mk.h) */
 #define ST_QUIESCENT 1
@@ -639,6 +640,10 @@ typedef struct {
     int call_open, call_dep;
     int64_t call_x;
     uint32_t call_steps;
+    /* a call imported mid-slice (orc_session_import): instructions its
+     * slice has already retired, and where the round stands */
+    uint32_t slice_carry;
+    int res_pos, res_changed;
 } lane_t;
 
 enum { R_NONE = 0, R_CHANGED = 1, R_RETIRED = 3, R_OVERFLOW = 4 };
@@ -1105,6 +1110,8 @@ static void lane_reset_session(const orc_net *net, lane_t *ln)
     ln->call_open = ln->call_dep = 0;
     ln->call_x = 0;
     ln->call_steps = 0;
+    ln->slice_carry = 0;
+    ln->res_pos = ln->res_changed = 0;
 }
 
 /* One slice of a /compute call: a new call with input *x, or (x == NULL)
@@ -1127,27 +1134,33 @@ static uint8_t session_step(const orc_net *net, lane_t *ln, const int64_t *x, ui
         ln->call_x = *x;
         ln->call_steps = 0;
     }
-    const uint32_t s0 = ln->steps;
+    const uint32_t s0 = ln->steps, carry = ln->slice_carry;
+    ln->slice_carry = 0;
     uint8_t st;
     for (;;) {
-        if (!ln->call_dep && !ln->in_avail) {
-            ln->in_avail = 1;
-            ln->in_val = ln->call_x;
-            ln->call_dep = 1;
+        /* an imported call may stand inside a round: finish that round first */
+        const int n0 = ln->res_pos;
+        int changed = ln->res_changed, over = 0;
+        ln->res_pos = ln->res_changed = 0;
+        if (n0 == 0) {
+            if (!ln->call_dep && !ln->in_avail) {
+                ln->in_avail = 1;
+                ln->in_val = ln->call_x;
+                ln->call_dep = 1;
+            }
+            if (ln->call_dep && ln->out_full) {
+                ln->out_full = 0;
+                *out = (int32_t)ln->out_val;
+                st = ST_HAS_OUTPUT;
+                ln->call_open = 0;
+                break;
+            }
+            if (ln->steps - s0 + carry >= budget) {
+                st = ST_BUDGET; /* the call stays open */
+                break;
+            }
         }
-        if (ln->call_dep && ln->out_full) {
-            ln->out_full = 0;
-            *out = (int32_t)ln->out_val;
-            st = ST_HAS_OUTPUT;
-            ln->call_open = 0;
-            break;
-        }
-        if (ln->steps - s0 >= budget) {
-            st = ST_BUDGET; /* the call stays open */
-            break;
-        }
-        int changed = 0, over = 0;
-        for (int n = 0; n < net->nprog; n++) {
+        for (int n = n0; n < net->nprog; n++) {
             int r = attempt(net, ln, n);
             if (r & R_OVERFLOW) {
                 over = 1;
@@ -1250,6 +1263,48 @@ int orc_sessions_compute(orc_sessions *S, const int64_t *in, int32_t *out, uint8
         pthread_create(&tid[t], NULL, sworker, &jobs[t]);
     for (int t = 0; t < threads; t++)
         pthread_join(tid[t], NULL);
+    return 0;
+}
+
+/* A session's state in the interpreter's terms (mk_exec.hip's session
+ * arrays for one instance), with an open call: the native tier hands a call
+ * off at a superblock entry (sess_convert.h); the test infrastructure
+ * imports that state here and lets the oracle finish the call. */
+int orc_session_import(orc_sessions *S, size_t i, const orc_flat *f)
+{
+    if (!S || i >= S->n || !f) return -1;
+    lane_t *ln = S->lanes[i];
+    const orc_net *net = S->net;
+    for (int n = 0; n < net->nprog; n++) {
+        pnode_t *nd = &ln->node[n];
+        nd->acc = f->acc[n];
+        nd->bak = f->bak[n];
+        nd->ptr = f->ip[n];
+        for (int k = 0; k < 4; k++) {
+            nd->full[k] = (int)((f->pfull >> (4 * n + k)) & 1u);
+            nd->val[k] = f->port[4 * n + k];
+        }
+        nd->pend = (int)((f->pend >> n) & 1u);
+        nd->pendval = f->pendv[n];
+        nd->hung = (int)((f->hung >> n) & 1u);
+    }
+    for (int s = 0; s < net->nstack; s++) {
+        if (f->depth[s] > ln->stack_cap) return -1;
+        ln->stk[s].n = f->depth[s];
+        for (uint32_t d = 0; d < f->depth[s]; d++) ln->stk[s].v[d] = f->entries[(size_t)s * ln->stack_cap + d];
+    }
+    ln->in_avail = f->in_full;
+    ln->in_val = f->in_val;
+    ln->out_full = f->out_full;
+    ln->out_val = f->out_val;
+    ln->dead = 0;
+    ln->call_open = 1;
+    ln->call_dep = f->deposited;
+    ln->call_x = f->pin;
+    ln->call_steps = f->csteps;
+    ln->slice_carry = f->csteps;
+    ln->res_pos = f->pos;
+    ln->res_changed = f->changed;
     return 0;
 }
 

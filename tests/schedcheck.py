@@ -106,3 +106,70 @@ def tier(nodes, *, stack_cap=None, stop_on_output=False):
         return TIERS[t], why.value.decode()
     finally:
         lib().mkc_free(h)
+
+
+# ---- stateful sessions on the host model (tis_sched.h compile_session_schedule)
+
+HANDOFF = 0xFE
+
+
+class OrcFlat(C.Structure):
+    """oracle/orc_flat.h"""
+    _fields_ = [("acc", C.c_int64 * 64), ("bak", C.c_int64 * 64), ("ip", C.c_int32 * 64), ("pendv", C.c_int32 * 64),
+                ("port", C.c_int32 * 256), ("pfull", C.c_uint64), ("pend", C.c_uint32), ("hung", C.c_uint32),
+                ("in_full", C.c_int32), ("out_full", C.c_int32), ("in_val", C.c_int32), ("out_val", C.c_int32),
+                ("depth", C.c_uint32 * 64), ("entries", C.c_void_p), ("deposited", C.c_int32), ("pin", C.c_int32),
+                ("pos", C.c_int32), ("changed", C.c_int32), ("csteps", C.c_uint32)]
+
+
+class HostSessions:
+    """n session instances executing the session schedule's device form
+    (sched_check.cpp mkc_sess_*); ``call(values)`` is one /compute on each.
+    Calls that hand off report HANDOFF; ``export(i)`` is the state the
+    interpreter would continue from."""
+
+    def __init__(self, nodes, n, *, stack_cap=None):
+        h = lib()
+        h.mkc_sess_new.restype = C.c_void_p
+        h.mkc_sess_new.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]
+        h.mkc_sess_free.argtypes = [C.c_void_p]
+        h.mkc_sess_call.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        h.mkc_sess_export.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(OrcFlat), C.c_void_p]
+        self.cap = 1024 if stack_cap is None else stack_cap
+        self._net, self._keep = _load(nodes)
+        why = C.create_string_buffer(1 << 20)
+        self._h = h.mkc_sess_new(self._net, self.cap, n, why, len(why))
+        if not self._h:
+            lib().mkc_free(self._net)
+            self._net = None
+            raise NotCompiled(why.value.decode())
+        self.plan = why.value.decode()
+        self.n = n
+        self.nstack = 0
+
+    def call(self, values, *, budget=None):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64))
+        assert v.size == self.n
+        out = np.zeros(self.n, np.int32)
+        st = np.zeros(self.n, np.uint8)
+        sp = np.zeros(self.n, np.uint32)
+        rc = lib().mkc_sess_call(self._h, v.ctypes.data, budget or (1 << 20), out.ctypes.data, st.ctypes.data,
+                                 sp.ctypes.data)
+        assert rc == 0, f"emulator error {rc}"
+        return out, st, sp
+
+    def export(self, i, nstack):
+        f = OrcFlat()
+        ent = np.zeros(max(1, nstack) * self.cap, np.int32)
+        rc = lib().mkc_sess_export(self._h, i, C.byref(f), ent.ctypes.data)
+        assert rc == 0, f"export error {rc}"
+        f.entries = ent.ctypes.data
+        return f, ent
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().mkc_sess_free(self._h)
+            self._h = None
+        if getattr(self, "_net", None):
+            lib().mkc_free(self._net)
+            self._net = None

@@ -444,8 +444,9 @@ def test_c4_full_size_properties(gpu):
 
 
 # The other two C4 bench workloads at their bench sizes, through the default
-# heavy kernel (wave-blocked buffer slots: d256 1,864 slots x 8,192 waves,
-# d1024 8,008 slots x 4,096 waves = 8.4 GB): constant status and steps on
+# heavy kernel (d256: 193 shared slots, the first 160 in LDS and the rest in
+# the wave's HBM block; d1024: 961 shared slots in HBM, wave-blocked buffer
+# slots, 4,096 waves): constant status and steps on
 # every lane (the pipeline's control flow does not depend on x), the
 # counters, and a tail slice bit-exact against the oracle
 # (stack.go:95-155, intStack.go:20-38).
