@@ -173,10 +173,13 @@ def measured_profile(workload):
 
 def plan_signature(plan):
     """The executor fields a PMC profile must share with a run to describe it:
-    same kernel shape and stack slots (a profile of the HBM-slot kernel says
-    nothing about the LDS one, though both retire the same instructions)."""
+    same kernel shape, stack slots and generated source (a profile of the
+    HBM-slot kernel says nothing about the LDS one, though both retire the
+    same instructions)."""
     f = dict(w.split("=", 1) for w in plan.split() if "=" in w)
-    return f.get("tier"), f.get("shape"), f.get("slots")
+    # kernel: hash of the generated module source (a new code generator or
+    # layout is a new kernel, whose counters the old profile does not hold)
+    return f.get("tier"), f.get("shape"), f.get("slots"), f.get("kernel")
 
 
 def measured_traffic(workload):

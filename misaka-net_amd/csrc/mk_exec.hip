@@ -1390,6 +1390,7 @@ struct JitState {
     std::vector<char> code;   // gfx950 code object
     double compile_s = 0;
     size_t src_bytes = 0;
+    uint64_t src_hash = 0;    // FNV-1a of the module source: which kernel a profile describes
     JitShape shape = JIT_STREAM;
     uint64_t max_steps = UINT64_MAX; // stream shape: launches need budget > max_steps
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
@@ -2127,6 +2128,8 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     auto job = std::make_shared<HiprtcJob>();
     job->src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
     J.src_bytes = job->src.size();
+    J.src_hash = 0xcbf29ce484222325ull;
+    for (unsigned char ch : job->src) J.src_hash = (J.src_hash ^ ch) * 0x100000001b3ull;
     {
         std::lock_guard<std::mutex> lk(g_rtc_mu);
         ++g_rtc_running;
@@ -3132,8 +3135,8 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                        P.nregs, P.nslots, P.code.size(), P.jtab.size(), (unsigned long long)P.sym_rounds);
     std::string s;
     if (t == mk::TIER_NATIVE) {
-        char tail[160];
-        snprintf(tail, sizeof tail, " shape=%s%s source=%zuB code=%zuB compile=%.2fs rtc=%s",
+        char tail[200];
+        snprintf(tail, sizeof tail, " shape=%s%s source=%zuB kernel=%016llx code=%zuB compile=%.2fs rtc=%s",
                  sc->jit.shape == mk::JIT_MACHINE ? "machine"
                  : sc->jit.heavy                  ? (sc->jit.lds ? "stream-heavy-lds"
                                                      : sc->jit.lds_n ? "stream-heavy-split"
@@ -3142,7 +3145,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                  sc->jit.pool >= 64 ? ("-pool" + std::to_string(sc->jit.pool)).c_str()
                  : sc->jit.pool     ? ("-k" + std::to_string(sc->jit.pool)).c_str()
                                     : "",
-                 sc->jit.src_bytes,
+                 sc->jit.src_bytes, (unsigned long long)sc->jit.src_hash,
                  sc->jit.code.size(), sc->jit.compile_s, sc->jit.rtc.c_str());
         s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
     } else {

@@ -417,6 +417,28 @@ int mkc_sess_export(void *ev, size_t i, orc_flat *f, int32_t *entries)
     return bad ? -3 : 0;
 }
 
+// The session lane of the native tier (tis_jit.h jit_session_lane) for the
+// CPU tests: 0 with the source in `out` and the register / slot counts, 1
+// when the compiler declined (why in `out`), negative when `out` is too small.
+int mkc_sess_lane(void *hv, uint32_t cap, uint32_t *nregs, uint32_t *nslots, char *out, size_t out_len)
+{
+    auto *h = (CheckNet *)hv;
+    mk::SchedProgram P;
+    std::string w, src;
+    mk::SchedLimits lim;
+    int rc = 0;
+    if (!mk::compile_session_schedule(h->net, cap, lim, P, w) ||
+        !mk::jit_session_lane(P, mk::JitLimits::from_env(), src, w)) {
+        src = w;
+        rc = 1;
+    }
+    *nregs = P.nregs;
+    *nslots = P.nslots;
+    if (src.size() + 1 > out_len) return -1;
+    memcpy(out, src.c_str(), src.size() + 1);
+    return rc;
+}
+
 // Lane function of the native tier (tis_jit.h) for the CPU tests: returns 0
 // with the source in `out`, 1 when the schedule or the JIT declined (why in
 // `out`), negative when `out` is too small.

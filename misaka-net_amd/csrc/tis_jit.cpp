@@ -252,6 +252,12 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
                 leave = true;
                 break;
             case U_END: if (I.fl & UF_OUTREG) use(I.a); leave = true; break;
+            case U_YIELD: // sessions: a call ends; the next one starts at variant lo32(imm)
+                if (I.fl & UF_OUTREG) use(I.a);
+                ok = reach(v, (uint32_t)(uint64_t)I.imm);
+                leave = true;
+                break;
+            case U_HANDOFF: leave = true; break; // sessions: the interpreter goes on from this entry
             case U_GUARD: ok = reach(v, (uint64_t)I.imm); break;
             case U_ROUND_END: if (I.fl & UF_OUTREG) use(I.a); break;
             default: ok = false;
@@ -1390,6 +1396,12 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("#endif");
     e.line("#define MK_SB_DONE 0xFFFFFFFEu");
     e.line("#define MK_SB_IDLE 0xFFFFFFFFu");
+    if (p.session) {
+        e.line("#define MK_SS_HANDOFF 0xFEu");     // L.st of a lane handed to the interpreter
+        e.line("#define MK_SS_DEAD 0xFFFFFFF0u");  // session ended (stack overflow)
+        e.line("#define MK_SS_T1 0xFFFFFFF1u");    // the interpreter holds the session
+        e.line("#define MK_SS_HAND 0xFFFFFFF2u");  // handed off in this launch (tis_session_import converts it)
+    }
     {
         uint32_t used = 0;
         for (uint32_t r = 0; r < p.nregs; ++r) used += g.used_reg[r] ? 1u : 0u;
@@ -1406,7 +1418,23 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         if (g.used_reg[r]) e.line("    int64_t r%u;", r);
     e.line("    uint32_t sb, steps, st;");
     e.line("    int32_t outv;");
+    if (p.session) e.line("    uint32_t next; // sessions: where the next call starts (MK_SS_* markers)");
     e.line("};");
+    if (p.session) {
+        // the persistent lane state of a session between calls (mk_sess_exec):
+        // its registers, [register][session] in HBM
+        e.line("MK_FN void mk_sess_input(MkLane &L, int64_t x) { L.r%u = x; }", p.in_reg);
+        e.line("MK_FN void mk_sess_load(MkLane &L, const int64_t *regs, uint64_t i, uint64_t n, bool on)");
+        e.line("{");
+        for (uint32_t r = 0; r < p.nregs; ++r)
+            if (g.used_reg[r]) e.line("    L.r%u = on ? regs[%lluull * n + i] : 0;", r, (unsigned long long)r);
+        e.line("}");
+        e.line("MK_FN void mk_sess_store(const MkLane &L, int64_t *regs, uint64_t i, uint64_t n)");
+        e.line("{");
+        for (uint32_t r = 0; r < p.nregs; ++r)
+            if (g.used_reg[r]) e.line("    regs[%lluull * n + i] = L.r%u;", (unsigned long long)r, r);
+        e.line("}");
+    }
     e.line("MK_FN void mk_init(MkLane &L, int64_t in)");
     e.line("{");
     for (uint32_t r = 0; r < p.nregs; ++r)
@@ -1536,6 +1564,21 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             e.line("    L.st = %uu;", I.d);
             e.line("    L.sb = MK_SB_DONE;");
             break;
+        case U_YIELD: { // sessions: the call ends; the next starts at lo32(imm)
+            char o[64];
+            snprintf(o, sizeof o, "(int32_t)%" PRId32, (int32_t)((uint64_t)I.imm >> 32));
+            e.line("    L.steps += %uu;", I.inc);
+            e.line("    L.outv = %s;", (I.d & MK_ST_HAS_OUTPUT) ? ((I.fl & UF_OUTREG) ? w.result(I).c_str() : o) : "0");
+            e.line("    L.st = %uu;", I.d);
+            e.line("    L.next = %uu;", (uint32_t)(uint64_t)I.imm);
+            e.line("    L.sb = MK_SB_DONE;");
+            break;
+        }
+        case U_HANDOFF: // sessions: the interpreter finishes the call from this superblock's entry
+            e.line("    L.st = MK_SS_HANDOFF;");
+            e.line("    L.next = %uu;", (uint32_t)I.imm);
+            e.line("    L.sb = MK_SB_DONE;");
+            break;
         default: break;
         }
         e.line("    X%u:", v);
@@ -1560,6 +1603,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         e.line("    }");
     }
     e.line("}");
+    if (p.session) return; // sessions: mk_sess_exec drives mk_run; no single-lane form
     // the whole lane, for the CPU tests (the kernel drives mk_run itself)
     e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
@@ -2348,8 +2392,10 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 }
 )";
 
-std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
-                              uint32_t pool)
+namespace {
+// Everything a module needs before its lane code: types, status codes,
+// policy, the flag / loop helpers, the slot-access macros, mk_device_common.
+std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool)
 {
     Emitter e;
     if (shape == JIT_MACHINE && pool >= 64) e.line("#define MK_POOL %uu", pool);
@@ -2443,12 +2489,122 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     e.line("#define MK_KEEP(m, need) mk_keep(m, need)");
     e.s += kDeviceCommon;
     e.s += "\n";
+    return e.s;
+}
+
+// Stateful sessions (row f2): every thread one session instance, its lane
+// state (superblock to start the next call at, registers, stack slots)
+// loaded from and stored back to HBM; each of the launch's ncalls /compute
+// calls runs the session schedule's superblocks by generations (the
+// dispatcher of kMachineKernel) until the call yields.  A call whose budget
+// slice would end inside a superblock hands off (MK_SS_HANDOFF): the lane
+// stops at that superblock's entry, records it, and the interpreter
+// (mk_exec.hip tis_session_import + tis_session) finishes that call and the
+// rest of the burst.  Sessions the interpreter holds (MK_SS_T1) are skipped.
+const char *const kSessionKernel = R"(
+struct SessK {
+    uint64_t n;
+    uint32_t ncalls, budget;
+    const int64_t *in;   // [ncalls][n]
+    int32_t *out;        // [ncalls][n]
+    uint8_t *status;     // [ncalls][n]
+    uint32_t *steps;     // [ncalls][n] or null
+    uint32_t *sb;        // [n] variant the next call starts at, or MK_SS_*
+    int64_t *regs;       // [register][n]
+    int32_t *slots;      // [slot][n]
+    uint32_t *hand_sb;   // [n] superblock of a hand-off
+    uint32_t *hand_steps;// [n] the call's steps at it
+    uint32_t *hand_call; // [n] the call of the burst it happened in
+};
+extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
+{
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const bool live = gid < p.n;
+    uint32_t sbv = live ? p.sb[gid] : MK_SS_DEAD;
+    const bool native = sbv < MK_SS_DEAD;
+    MkLane L;
+    mk_sess_load(L, p.regs, gid, p.n, native);
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    for (uint32_t call = 0; call < p.ncalls; ++call) {
+        const uint64_t ci = (uint64_t)call * p.n + gid;
+        const bool run = sbv < MK_SS_DEAD;
+        L.sb = run ? sbv : MK_SB_IDLE;
+        L.steps = 0u;
+        L.st = 0u;
+        L.outv = 0;
+        L.next = MK_SS_DEAD;
+        if (run) mk_sess_input(L, (int64_t)(int32_t)p.in[ci]); // int32(v) at GetInput (master.go:237)
+        for (;;) {
+            const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
+            if (!actb) break;
+            const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
+            const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
+            if (L.sb == u) mk_run(u, L, p.budget, slots, p.n, MK_POLICY, smax);
+        }
+        if (!live || sbv == MK_SS_T1 || sbv == MK_SS_HAND) continue; // the interpreter answers these
+        if (run && L.st == MK_SS_HANDOFF) {
+            p.hand_sb[gid] = L.next / 2u;
+            p.hand_steps[gid] = L.steps;
+            p.hand_call[gid] = call;
+            sbv = MK_SS_HAND;
+            continue;
+        }
+        p.out[ci] = run && (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+        p.status[ci] = (uint8_t)(run ? L.st : MK_ST_STACK_OVERFLOW);
+        if (p.steps) p.steps[ci] = run ? L.steps : 0u;
+        if (run) sbv = L.next;
+    }
+    if (native) {
+        mk_sess_store(L, p.regs, gid, p.n);
+        p.sb[gid] = sbv;
+    }
+}
+)";
+} // namespace
+
+std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
+                              uint32_t pool)
+{
+    Emitter e;
+    e.s = module_prelude(shape, lim, pool);
     e.s += lane_src;
     const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
     else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;
     e.s += shape == JIT_MACHINE ? mk : heavy ? kStreamKernelHeavy : kStreamKernel;
     return e.s;
+}
+
+} // namespace mk
+
+namespace mk {
+
+bool jit_session_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why)
+{
+    if (!p.session) {
+        why = "not a session schedule";
+        return false;
+    }
+    Graph g;
+    if (!analyze(p, lim, g, why)) return false;
+    Emitter e;
+    emit_machine_lane(p, g, e);
+    src = module_prelude(JIT_MACHINE, lim, 0) + e.s + kSessionKernel;
+    return true;
+}
+
+bool jit_session_lane(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why)
+{
+    if (!p.session) {
+        why = "not a session schedule";
+        return false;
+    }
+    Graph g;
+    if (!analyze(p, lim, g, why)) return false;
+    Emitter e;
+    emit_machine_lane(p, g, e);
+    src = e.s;
+    return true;
 }
 
 } // namespace mk

@@ -198,4 +198,12 @@ constexpr size_t kJitPoolMaxVariants = 1024; // LDS histogram of parked lanes pe
 // MK_JIT_SLOT_LAYOUT=blocked|lane forces one.
 constexpr uint32_t kJitWaveBlockedSlots = 1u << 22;
 
+// Stateful sessions (row f2): the session schedule (compile_session_schedule)
+// as a machine-shape lane plus the kernel kJitSessKernel, one thread per
+// session, state in HBM; handed-off calls go to the interpreter.
+constexpr const char *kJitSessKernel = "mk_sess_exec";
+bool jit_session_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why);
+// The lane part alone (CPU tests compile it with g++).
+bool jit_session_lane(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why);
+
 } // namespace mk

@@ -173,3 +173,20 @@ class HostSessions:
         if getattr(self, "_net", None):
             lib().mkc_free(self._net)
             self._net = None
+
+
+def session_lane(nodes, *, stack_cap=None):
+    """(session lane source of the native tier, registers, stack slots)."""
+    h, _keep = _load(nodes)
+    try:
+        lib().mkc_sess_lane.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                        C.c_char_p, C.c_size_t]
+        nr, ns = C.c_uint32(), C.c_uint32()
+        buf = C.create_string_buffer(1 << 24)
+        rc = lib().mkc_sess_lane(h, 1024 if stack_cap is None else stack_cap, C.byref(nr), C.byref(ns), buf, len(buf))
+        if rc == 1:
+            raise NotCompiled(buf.value.decode())
+        assert rc == 0, rc
+        return buf.value.decode(), nr.value, ns.value
+    finally:
+        lib().mkc_free(h)

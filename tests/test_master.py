@@ -381,7 +381,7 @@ def test_quiescent_call_then_next_input():
     # BASELINE config 3's network: zero has no output (504 at once, the
     # instance lives on), then 5 doubles
     progs = {s.name: s.program for s in mk.networks.sample_network() if s.kind == "program"}
-    m = _stateful(progs)
+    m = _stateful(progs, name="master")
     assert _compute(m, 0) == (504, "network produced no output\n")
     assert _compute(m, 5) == (200, '{"value":10}\n')
 
@@ -414,7 +414,8 @@ def test_http_long_call_on_the_gpu(gpu):
 @pytest.mark.gpu
 def test_http_c3_zero_then_five(gpu):
     nodes = mk.networks.sample_network()
-    m = MasterNode({s.name: {"type": s.kind} for s in nodes}, {s.name: s.program for s in nodes if s.kind == "program"})
+    m = MasterNode({s.name: {"type": s.kind} for s in nodes if s.kind != "master"},
+                   {s.name: s.program for s in nodes if s.kind == "program"}, name="master")
     srv = make_server(m, port=0)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
     port = srv.server_address[1]

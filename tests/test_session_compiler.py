@@ -122,3 +122,105 @@ def test_stack_loop_networks(seed):
                  kind=gen.get("kind", 0), mask=gen.get("mask", 0))
     except NotCompiled:
         pytest.skip("not compilable")
+
+
+# ---- the generated session lane (tis_jit.cpp, machine shape) compiled with g++,
+# driven like mk_sess_exec drives it, against the host model call by call
+
+SESS_HEADER = """#include <cstdint>
+#include <cstddef>
+#define MK_FN static inline
+#define MK_LOOP_NEED(pol) 0u
+#define MK_KEEP(m, need) (m)
+#define MK_ALL(p) (p)
+#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))
+#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])
+#define MK_SLOT_STX(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))
+#define MK_SLOT_LDX(b, ss, s) ((b)[(uint64_t)(s) * (ss)])
+#define MK_FLAG_GT(x) ((int32_t)((x) > 0))
+#define MK_FLAG_LT(x) ((int32_t)((x) < 0))
+#define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
+#define MK_FLAG_MIN(x, f) ((int32_t)((uint32_t)(x) < (uint32_t)(f) ? (uint32_t)(x) : (uint32_t)(f)))
+#define MK_MAD24(f, k, x) ((int32_t)((uint32_t)(x) + (uint32_t)(f) * (uint32_t)(k)))
+"""
+
+SESS_DRIVER = """
+extern "C" void sessrun{i}(size_t n, uint32_t budget, const int64_t *in, int32_t *out, uint8_t *st, uint32_t *sp,
+                          uint32_t *sb, int64_t *regs, int32_t *slots) {{
+    using namespace n{i};
+    for (size_t s = 0; s < n; s++) {{
+        MkLane L;
+        mk_sess_load(L, regs, s, n, sb[s] < MK_SS_DEAD);
+        out[s] = 0; sp[s] = 0;
+        if (sb[s] == MK_SS_DEAD) {{ st[s] = 3; continue; }}
+        if (sb[s] >= MK_SS_DEAD) {{ st[s] = 0xFE; continue; }}
+        L.sb = sb[s]; L.steps = 0; L.st = 0; L.outv = 0; L.next = MK_SS_DEAD;
+        mk_sess_input(L, (int64_t)(int32_t)in[s]);
+        while (L.sb < MK_SB_DONE) mk_run(L.sb, L, budget, slots + s, n, 0u, L.steps);
+        if (L.st == MK_SS_HANDOFF) {{ st[s] = 0xFE; sp[s] = L.steps; sb[s] = MK_SS_HAND; }}
+        else {{ out[s] = (L.st & 0x10) ? L.outv : 0; st[s] = (uint8_t)L.st; sp[s] = L.steps; sb[s] = L.next; }}
+        mk_sess_store(L, regs, s, n);
+    }}
+}}
+"""
+
+
+def _build_sessions(cases, path):
+    import ctypes as C
+    import subprocess
+
+    parts = [SESS_HEADER]
+    for i, (src, _nr, _ns) in enumerate(cases):
+        parts.append(f"namespace n{i} {{\n{src}\n}}\n")
+        parts.append(SESS_DRIVER.format(i=i))
+    with open(path + ".cpp", "w") as f:
+        f.write("".join(parts))
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-w", "-o", path + ".so", path + ".cpp"])
+    return C.CDLL(path + ".so")
+
+
+def test_generated_session_lane(tmp_path):
+    import schedcheck as sc
+
+    nets = [("example", mk.networks.example_network(), {}, (0, 0)),
+            ("sample", mk.networks.sample_network(), {}, (0, 0)),
+            ("countdown", mk.networks.countdown_network(), {"budget": 700}, (1, 1023)),
+            ("pipeline8", mk.networks.pipeline_network(8), {}, (0, 0)),
+            ("sum", [("n", "program", "IN NIL\nADD 10\nOUT ACC")], {}, (0, 0)),
+            ("twice", [("n", "program", "IN ACC\nOUT ACC\nOUT ACC")], {}, (0, 0)),
+            ("ovf", [("n", "program", "IN ACC\nPUSH ACC, s\nPOP s, ACC\nPUSH ACC, s\nOUT ACC"), ("s", "stack", "")],
+             {"stack_cap": 3}, (0, 0))]
+    for seed in range(30):
+        nets.append((f"rand{seed}", random_network(seed), {"budget": [37, 200, 1000][seed % 3],
+                                                          "stack_cap": [1, 3, 8, 16, 17, 40, 1024][seed % 7]}, (0, 0)))
+    for seed in range(12):
+        rows, gen = stack_loop_network(seed)
+        nets.append((f"stk{seed}", rows, {"budget": [100, 2000][seed % 2]}, (gen["kind"], gen["mask"])))
+    cases, keep = [], []
+    for label, nodes, kw, gen in nets:
+        try:
+            cases.append(sc.session_lane(nodes, stack_cap=kw.get("stack_cap")))
+            keep.append((label, nodes, kw, gen))
+        except NotCompiled:
+            pass
+    lib = _build_sessions(cases, str(tmp_path / "sess"))
+    import ctypes as C
+
+    n = 16
+    for i, ((label, nodes, kw, gen), (src, nr, ns)) in enumerate(zip(keep, cases)):
+        host = HostSessions(nodes, n, stack_cap=kw.get("stack_cap"))
+        sb = np.zeros(n, np.uint32)
+        regs = np.zeros(max(1, nr) * n, np.int64)
+        slots = np.full(max(1, ns) * n, 0x5A5A5A5A, np.int32)
+        b = kw.get("budget") or (1 << 20)
+        for k in range(5):
+            row = po.gen_inputs(k * 31 + i, n, kind=gen[0], mask=gen[1])
+            ref = host.call(row, budget=b)
+            out, st, sp = np.zeros(n, np.int32), np.zeros(n, np.uint8), np.zeros(n, np.uint32)
+            getattr(lib, f"sessrun{i}")(C.c_size_t(n), C.c_uint32(b), C.c_void_p(row.ctypes.data),
+                                        C.c_void_p(out.ctypes.data), C.c_void_p(st.ctypes.data),
+                                        C.c_void_p(sp.ctypes.data), C.c_void_p(sb.ctypes.data),
+                                        C.c_void_p(regs.ctypes.data), C.c_void_p(slots.ctypes.data))
+            for a, r in zip((out, st, sp), ref):
+                bad = np.nonzero(a != r)[0]
+                assert not bad.size, (label, k, int(bad[0]), int(a[bad[0]]), int(r[bad[0]]))

@@ -10,6 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 for m in st4 ld4 ld16; do
   timeout -k 10 60 ./tools/probe/pmc_calib $m $MIB > "$OUT/$m.json" || { echo "[calib] $m failed"; exit 1; }
+  mkdir -p "$OUT/$m"
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "[calib] $(date +%T) $m $c"
     timeout -s KILL 60 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/$m/$c" -o p -- ./tools/probe/pmc_calib $m $MIB > "$OUT/$m/$c.log" 2>&1 || { echo "[calib] failed $m $c"; tail -5 "$OUT/$m/$c.log"; exit 1; }
