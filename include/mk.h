@@ -262,6 +262,16 @@ int mk_net_node_index(const mk_net *net, const char *name, int *kind, int *index
  * an input not deposited yet is dropped.  Synchronous. */
 int mk_session_cancel(mk_session *s);
 
+/* Which tier runs the sessions, as one line of text: "tier=native ..." --
+ * the network's session schedule compiled to a kernel (one thread per
+ * session, state in HBM; a call whose budget slice ends inside a superblock
+ * is handed to the interpreter, which keeps that session) -- or
+ * "tier=interp reason=..." (the bytecode interpreter for every session:
+ * mixed deployments, networks the compiler declines, MK_SESSION_NATIVE=0).
+ * Host-side state access (mk_session_port_put, _stack_*, _input_take,
+ * _output_put) is for interpreter sessions: MK_EINVAL on the native tier. */
+int mk_session_plan(const mk_session *s, char *out, size_t out_len);
+
 /* /reset (master.go:126-143): every session back to the initial state. */
 int mk_session_reset(mk_session *s);
 

@@ -123,6 +123,7 @@ SIGNATURES = {
     "mk_session_compute_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_reset": (C.c_int, [C.c_void_p]),
     "mk_session_cancel": (C.c_int, [C.c_void_p]),
+    "mk_session_plan": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "mk_session_free": (None, [C.c_void_p]),
     "mk_generate_inputs_device": (
         C.c_int,

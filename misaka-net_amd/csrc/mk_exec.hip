@@ -59,10 +59,15 @@ extern char **environ;
 #include "tis_front.h"
 #include "tis_jit.h"
 #include "tis_sched.h"
+#define MK_HD __host__ __device__
+#include "sess_convert.h"
 
 namespace mk {
 
 constexpr int kBlock = 256;
+// Native sessions' markers (tis_jit.cpp MK_SS_*; 0xFFFFFFF0 = ended): held by
+// the interpreter, handed off in this launch.
+constexpr uint32_t kSessT1 = 0xFFFFFFF1u, kSessHand = 0xFFFFFFF2u;
 constexpr int kMaxDevices = 64;
 
 struct KParams {
@@ -953,6 +958,13 @@ struct SessParams {
     uint32_t *csteps;   // [n] steps retired by the current call so far
     uint32_t mixed;     // network has remote peers: a round without change parks the call
     uint32_t resume;    // continue each session's parked call (in ignored)
+    // native sessions (tis_jit.h mk_sess_exec): the interpreter runs only the
+    // sessions marked MK_SS_T1 here (null: all).  One handed off in this
+    // launch (io bit 8, set by tis_session_import) starts at its call
+    // hand_call[i], resumed, its step count that of the native slice, at
+    // round position io bits 9-13 with io bit 14 "something changed".
+    const uint32_t *nsb;       // [n]
+    const uint32_t *hand_call; // [n]
 };
 
 template <int NMAX>
@@ -965,7 +977,7 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     const uint64_t n = p.n;
     int32_t *const port = lds;                     // [nprog*4][B]
     int32_t *const sdepth = lds + p.nprog * 4 * B; // [nstack][B]
-    const bool live = gid < n;
+    const bool live = gid < n && (!p.nsb || p.nsb[gid] == kSessT1);
 
     int64_t acc[NMAX], bak[NMAX];
     int32_t ip[NMAX], pendv[NMAX], xval[NMAX];
@@ -996,6 +1008,8 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     }
     bool in_full = io & 1u, out_full = (io >> 1) & 1u;
     uint32_t dead = (io >> 4) & 15u;
+    const bool fresh = live && ((io >> 8) & 1u); // handed off by the native tier in this launch
+    const uint32_t c0 = fresh ? p.hand_call[gid] : 0u;
     // ncalls sequential /compute calls, the state carried in registers/LDS
     // from one to the next (a burst of requests on one instance, one launch)
     for (uint32_t call = 0; call < p.ncalls; ++call) {
@@ -1005,19 +1019,25 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     // continues it with its input and step count; a new call while one is
     // open does nothing and reports MK_ST_CALL_OPEN (tis_oracle.c session_step)
     const bool open = live && ((io >> 3) & 1u);
-    const bool resumed = p.resume && open;
-    const bool ran = live && dead == 0 && (p.resume ? resumed : !open);
+    // a call the native tier handed off continues here (its earlier calls
+    // of the burst were answered by the native kernel)
+    const bool handed = fresh && call == c0, skip = fresh && call < c0;
+    const bool resumed = (p.resume || handed) && open;
+    const bool ran = live && !skip && dead == 0 && (p.resume || handed ? resumed : !open);
     const int32_t x = !live ? 0 : resumed ? p.pin[gid] : (int32_t)p.in[ci]; // int32(v) at GetInput (master.go:237)
     bool active = ran, got = false;
     bool deposited = resumed && !((io >> 2) & 1u);
     int32_t result = 0;
     uint32_t steps = resumed ? p.csteps[gid] : 0u;
-    const uint32_t slice0 = steps;
+    const uint32_t slice0 = handed ? 0u : steps; // a handed-off call is still in its first slice
     bool parked = false; // the call stays open
     uint32_t reason = 0;
+    // where the hand-off stood inside a round: finish that round first
+    int first_pos = handed ? (int)((io >> 9) & 31u) : 0;
+    bool first_changed = handed && ((io >> 14) & 1u);
 
     for (;;) {
-        if (active) {
+        if (active && first_pos == 0) {
             if (!deposited && !in_full) {
                 in_full = true;
                 in_val = x;
@@ -1035,12 +1055,15 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
             }
         }
         if (!__ballot(active)) break;
-        bool changed = false, over = false;
+        bool changed = first_changed, over = false;
+        const int pos0 = first_pos;
+        first_pos = 0;
+        first_changed = false;
 #pragma unroll
         for (int k = 0; k < NMAX; ++k) {
             if (k >= p.nprog) continue; // wave-uniform
             const uint32_t len = p.len[k];
-            bool pending = active && !over && !((hung >> k) & 1u);
+            bool pending = active && !over && !((hung >> k) & 1u) && k >= pos0;
             unsigned long long todo = __ballot(pending);
             while (todo) {
                 const int lead = __builtin_ctzll(todo);
@@ -1199,7 +1222,7 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
             }
         }
     }
-    if (live) {
+    if (live && !skip) {
         p.out[ci] = got ? result : 0;
         p.status[ci] = (uint8_t)(got ? MK_ST_HAS_OUTPUT : ran ? reason : dead ? dead : open && !p.resume ? MK_ST_CALL_OPEN : 0u);
         if (p.steps) p.steps[ci] = ran ? steps : 0u;
@@ -1245,6 +1268,64 @@ __global__ void __launch_bounds__(kBlock) tis_session_cancel(uint32_t *io, uint6
 {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) io[i] &= ~0xCu;
+}
+
+// Native sessions handed off in this launch (MK_SS_HAND: a call's budget
+// slice ends inside a superblock) become interpreter sessions: the state
+// map of that superblock's entry (tis_sched.h SessMapHdr, from the schedule
+// compiler) with the lane's registers and stack slots, in the interpreter's
+// arrays (sess_convert.h), the call open and continuing its slice.
+struct SessImport {
+    uint64_t n;
+    int nprog, nstack;
+    uint32_t *nsb;
+    const uint32_t *hand_sb, *hand_steps;
+    const int64_t *regs;  // [register][n]
+    const int32_t *slots; // [slot][n]
+    const SessMapHdr *hdr;
+    const SessSrcDev *rec;
+    const int64_t *dyn_base;
+};
+
+struct SessImportOut {
+    const SessParams &p;
+    uint64_t i, n;
+    uint32_t io = 0;
+    __device__ void acc(int k, int64_t v) { p.acc[(uint64_t)k * n + i] = v; }
+    __device__ void bak(int k, int64_t v) { p.bak[(uint64_t)k * n + i] = v; }
+    __device__ void ip(int k, int32_t v) { p.ip[(uint64_t)k * n + i] = v; }
+    __device__ void pendv(int k, int32_t v) { p.pendv[(uint64_t)k * n + i] = v; }
+    __device__ void port(int q, int32_t v) { p.port[(uint64_t)q * n + i] = v; }
+    __device__ void pfull(uint64_t x) { p.pfull[i] = x; }
+    __device__ void bits(uint32_t pend, uint32_t hung) { p.bits[i] = (pend & 0xffffu) | (hung << 16); }
+    __device__ void chans(bool in_full, bool out_full, int32_t iv, int32_t ov)
+    {
+        io |= (in_full ? 1u : 0u) | (out_full ? 2u : 0u);
+        p.in_val[i] = iv;
+        p.out_val[i] = ov;
+    }
+    __device__ void depth(int s, uint32_t d) { p.sdepth[(uint64_t)s * n + i] = (int32_t)d; }
+    __device__ void entry(int s, uint32_t d, int32_t v) { p.stk[((uint64_t)s * p.stack_cap + d) * n + i] = v; }
+    __device__ void call(bool dep, int32_t pin, int pos, bool changed)
+    {
+        io |= 8u | 0x100u | (dep ? 0u : 4u) | ((uint32_t)pos << 9) | (changed ? 0x4000u : 0u);
+        p.pin[i] = pin;
+    }
+};
+
+__global__ void __launch_bounds__(kBlock) tis_session_import(SessImport q, SessParams p)
+{
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (gid >= q.n || q.nsb[gid] != kSessHand) return;
+    const SessMapHdr h = q.hdr[q.hand_sb[gid]];
+    const uint64_t n = q.n;
+    auto reg = [&](uint32_t r) { return q.regs[(uint64_t)r * n + gid]; };
+    auto slot = [&](uint32_t s) { return q.slots[(uint64_t)s * n + gid]; };
+    SessImportOut o{p, gid, n};
+    sess_convert(q.nprog, q.nstack, h, q.rec + h.off, q.dyn_base, reg, slot, o);
+    p.io[gid] = o.io;
+    p.csteps[gid] = q.hand_steps[gid];
+    q.nsb[gid] = kSessT1;
 }
 
 // ---- input order for the machine shape (tier 3) -----------------------------
@@ -2098,6 +2179,43 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     g_rtc_cv.notify_all();
 }
 
+uint64_t src_hash(const std::string &src)
+{
+    uint64_t h = 0xcbf29ce484222325ull; // FNV-1a
+    for (unsigned char ch : src) h = (h ^ ch) * 0x100000001b3ull;
+    return h;
+}
+
+// One module through hiprtc_run on a helper thread, abandoned after max_s
+// seconds (`why` says so).  `from` = which compiler built it.
+bool rtc_compile(const std::string &src, double max_s, std::vector<char> &code, std::string &why, std::string &from)
+{
+    auto job = std::make_shared<HiprtcJob>();
+    job->src = src;
+    {
+        std::lock_guard<std::mutex> lk(g_rtc_mu);
+        ++g_rtc_running;
+    }
+    std::thread(hiprtc_run, job).detach();
+    std::unique_lock<std::mutex> lk(job->mu);
+    const auto limit = std::chrono::duration<double>(max_s);
+    if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+        job->abandoned = true; // a helper child is killed; an in-process compile runs out
+        if (job->pid > 0) (void)kill(job->pid, SIGKILL);
+        char b[128];
+        snprintf(b, sizeof b, "hiprtc did not finish within the native tier's compile bound (%.0f s)", max_s);
+        why = b;
+        return false;
+    }
+    if (!job->ok) {
+        why = job->why;
+        return false;
+    }
+    code = std::move(job->code);
+    from = job->why; // the compiler whose module this is (hiprtc_run)
+    return true;
+}
+
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
 // gfx950); the code object is loaded per device on first use.  Bounded:
 // a lane source over lim.max_src_bytes is not compiled, and a compile that
@@ -2125,35 +2243,10 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, L);
     J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, L) : 0u;
     J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
-    auto job = std::make_shared<HiprtcJob>();
-    job->src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
-    J.src_bytes = job->src.size();
-    J.src_hash = 0xcbf29ce484222325ull;
-    for (unsigned char ch : job->src) J.src_hash = (J.src_hash ^ ch) * 0x100000001b3ull;
-    {
-        std::lock_guard<std::mutex> lk(g_rtc_mu);
-        ++g_rtc_running;
-    }
-    std::thread(hiprtc_run, job).detach();
-    {
-        std::unique_lock<std::mutex> lk(job->mu);
-        const auto limit = std::chrono::duration<double>(lim.max_compile_s);
-        if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
-            job->abandoned = true; // a helper child is killed; an in-process compile runs out
-            if (job->pid > 0) (void)kill(job->pid, SIGKILL);
-            char b[128];
-            snprintf(b, sizeof b, "hiprtc did not finish within the native tier's compile bound (%.0f s)",
-                     lim.max_compile_s);
-            J.why = b;
-            return false;
-        }
-        if (!job->ok) {
-            J.why = job->why;
-            return false;
-        }
-        J.code = std::move(job->code);
-        J.rtc = job->why; // the compiler whose module this is (hiprtc_run)
-    }
+    const std::string src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
+    J.src_bytes = src.size();
+    J.src_hash = src_hash(src);
+    if (!rtc_compile(src, lim.max_compile_s, J.code, J.why, J.rtc)) return false;
     if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded
         if (FILE *f = std::fopen(d, "wb")) {
             std::fwrite(J.code.data(), 1, J.code.size(), f);
@@ -2440,19 +2533,49 @@ struct mk_session {
     size_t stage_bytes = 0;
     hipStream_t stream = nullptr;
     mk::SessParams p{};
+    // native tier (tis_jit.h mk_sess_exec): the session schedule compiled to
+    // a kernel; the interpreter's state above holds the sessions handed to it
+    bool native = false;
+    std::string plan; // mk_session_plan
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    void *d_native = nullptr; // every native array, one allocation
+    size_t native_bytes = 0;
+    uint32_t *nsb = nullptr, *hand_sb = nullptr, *hand_steps = nullptr, *hand_call = nullptr;
+    int64_t *regs = nullptr;
+    int32_t *slots = nullptr;
+    mk::SessMapHdr *hdr = nullptr;
+    mk::SessSrcDev *rec = nullptr;
+    int64_t *dyn_base = nullptr;
     ~mk_session()
     {
         mk::DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipFree(d_state);
+        (void)hipFree(d_native);
         (void)hipFree(d_stage);
         (void)hipHostFree(h_stage);
+        if (mod) (void)hipModuleUnload(mod);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
 
 namespace mk {
 namespace {
+
+// Parameters of the native session kernel (tis_jit.cpp kSessionKernel's SessK).
+struct SessK {
+    uint64_t n;
+    uint32_t ncalls, budget;
+    const int64_t *in;
+    int32_t *out;
+    uint8_t *status;
+    uint32_t *steps;
+    uint32_t *sb;
+    int64_t *regs;
+    int32_t *slots;
+    uint32_t *hand_sb, *hand_steps, *hand_call;
+};
 
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
                    hipStream_t stream, uint32_t ncalls = 1, bool resume = false)
@@ -2469,10 +2592,103 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
     const size_t lds = (size_t)(s->nprog * 4 + s->nstack) * kBlock * 4;
     const uint64_t blocks = (s->n + kBlock - 1) / kBlock;
     if (blocks > 0x7fffffffull) return MK_ELIMIT;
+    if (s->native && !resume) {
+        // 1. the native kernel: every session it holds, every call of the burst
+        SessK k{s->n, ncalls, p.budget, d_in, d_out, d_status, d_steps, s->nsb, s->regs, s->slots,
+                s->hand_sb, s->hand_steps, s->hand_call};
+        void *kargs[] = {(void *)&k};
+        if (hipModuleLaunchKernel(s->fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr) !=
+            hipSuccess)
+            return MK_EDEVICE;
+        // 2. calls it handed off become interpreter sessions
+        SessImport q{s->n, s->nprog, s->nstack, s->nsb, s->hand_sb, s->hand_steps, s->regs, s->slots,
+                     s->hdr, s->rec, s->dyn_base};
+        void *iargs[] = {(void *)&q, (void *)&p};
+        if (hipLaunchKernel(reinterpret_cast<void *>(&tis_session_import), dim3((unsigned)blocks), dim3(kBlock), iargs,
+                            0, stream) != hipSuccess)
+            return MK_EDEVICE;
+    }
+    // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
     if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)blocks), dim3(kBlock), args, lds, stream) !=
         hipSuccess)
         return MK_EDEVICE;
+    return MK_OK;
+}
+
+// The native tier for a session set (row f2): the session schedule
+// (compile_session_schedule), its kernel (jit_session_source + hiprtc), the
+// state maps of its superblocks and the per-session lane state.  A network
+// the compiler or the native tier declines keeps the interpreter, with the
+// reason in s->plan; so does MK_SESSION_NATIVE=0.  Allocation failures are
+// errors.
+int session_native(mk_session *s)
+{
+    mk_net *h = s->h;
+    auto decline = [&](const std::string &why) {
+        s->plan = "tier=interp reason=" + why;
+        return MK_OK;
+    };
+    if (const char *e = std::getenv("MK_SESSION_NATIVE"); e && !std::strcmp(e, "0"))
+        return decline("disabled by MK_SESSION_NATIVE=0");
+    if (h->jit_lim.disabled) return decline("disabled by MK_JIT=0");
+    SchedProgram P;
+    std::string why, src, from;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (!compile_session_schedule(h->net, s->cap, SchedLimits{}, P, why)) return decline(why);
+        if (!jit_session_source(P, h->jit_lim, src, why)) return decline(why);
+    }
+    if (src.size() > h->jit_lim.max_src_bytes) return decline("session source over the native tier's size bound");
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<char> code;
+    if (!rtc_compile(src, h->jit_lim.max_compile_s, code, why, from)) return decline(why);
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    DeviceGuard g(s->device);
+    if (hipModuleLoadData(&s->mod, code.data()) != hipSuccess ||
+        hipModuleGetFunction(&s->fn, s->mod, kJitSessKernel) != hipSuccess)
+        return MK_EDEVICE;
+    std::vector<SessMapHdr> hdr;
+    std::vector<SessSrcDev> rec;
+    build_sess_map(P, s->nprog, s->nstack, hdr, rec);
+    const size_t N = s->n ? s->n : 1;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t sz[] = {al(N * 4), al((size_t)P.nregs * N * 8), al((size_t)std::max<uint32_t>(P.nslots, 1) * N * 4),
+                         al(N * 4), al(N * 4), al(N * 4), al(hdr.size() * sizeof(SessMapHdr)),
+                         al(rec.size() * sizeof(SessSrcDev)), al(std::max<size_t>(P.dyn_base.size(), 1) * 8)};
+    size_t total = 0;
+    for (size_t b : sz) total += b;
+    if (hipMalloc(&s->d_native, total) != hipSuccess) return MK_ENOMEM;
+    s->native_bytes = total;
+    char *b = (char *)s->d_native;
+    size_t off = 0;
+    auto take = [&](size_t i) { char *q = b + off; off += sz[i]; return q; };
+    s->nsb = (uint32_t *)take(0);
+    s->regs = (int64_t *)take(1);
+    s->slots = (int32_t *)take(2);
+    s->hand_sb = (uint32_t *)take(3);
+    s->hand_steps = (uint32_t *)take(4);
+    s->hand_call = (uint32_t *)take(5);
+    s->hdr = (SessMapHdr *)take(6);
+    s->rec = (SessSrcDev *)take(7);
+    s->dyn_base = (int64_t *)take(8);
+    // the maps never change: copied once (reset clears only the lane state)
+    if ((!hdr.empty() && hipMemcpy(s->hdr, hdr.data(), hdr.size() * sizeof(SessMapHdr), hipMemcpyHostToDevice) !=
+                             hipSuccess) ||
+        (!rec.empty() && hipMemcpy(s->rec, rec.data(), rec.size() * sizeof(SessSrcDev), hipMemcpyHostToDevice) !=
+                             hipSuccess) ||
+        (!P.dyn_base.empty() &&
+         hipMemcpy(s->dyn_base, P.dyn_base.data(), P.dyn_base.size() * 8, hipMemcpyHostToDevice) != hipSuccess))
+        return MK_EDEVICE;
+    s->native_bytes = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5]; // the lane state: what a reset clears
+    s->native = true;
+    s->p.nsb = s->nsb;
+    s->p.hand_call = s->hand_call;
+    char line[256];
+    snprintf(line, sizeof line, "tier=native superblocks=%u regs=%u slots=%u words=%zu source=%zuB kernel=%016llx "
+             "compile=%.2fs rtc=%s", P.nsb, P.nregs, P.nslots, P.code.size(), src.size(),
+             (unsigned long long)src_hash(src), secs, from.c_str());
+    s->plan = line;
     return MK_OK;
 }
 
@@ -2711,6 +2927,10 @@ int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_s
     p.mixed = h->net.uses_remote ? 1u : 0u;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return MK_EDEVICE;
     if (hipMemsetAsync(s->d_state, 0, total, s->stream) != hipSuccess) return MK_EDEVICE; // post-/reset state
+    int rc = mk::session_native(s.get());
+    if (rc) return rc;
+    if (s->native_bytes && hipMemsetAsync(s->d_native, 0, s->native_bytes, s->stream) != hipSuccess)
+        return MK_EDEVICE; // every session at the session schedule's first variant
     if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
     *out = s.release();
     return MK_OK;
@@ -2722,6 +2942,7 @@ int mk_session_reset(mk_session *s)
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     if (hipMemsetAsync(s->d_state, 0, s->state_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
+    if (s->native && hipMemsetAsync(s->d_native, 0, s->native_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
     return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 
@@ -2891,6 +3112,7 @@ int mk_session_remote_done(mk_session *s, size_t inst, uint32_t node, int32_t va
 int mk_session_port_put(mk_session *s, size_t inst, uint32_t node, uint32_t reg, int32_t value)
 {
     if (!s || inst >= s->n || node >= (uint32_t)s->nprog || reg > 3) return MK_EINVAL;
+    if (s->native) return MK_EINVAL; // host-side state access: interpreter sessions (mixed networks) only
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     const uint32_t q = node * 4 + reg;
@@ -2905,6 +3127,7 @@ int mk_session_port_put(mk_session *s, size_t inst, uint32_t node, uint32_t reg,
 int mk_session_stack_push(mk_session *s, size_t inst, uint32_t stack, int32_t value)
 {
     if (!s || inst >= s->n || stack >= (uint32_t)s->nstack) return MK_EINVAL;
+    if (s->native) return MK_EINVAL; // host-side state access: interpreter sessions (mixed networks) only
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     int32_t d = 0;
@@ -2918,6 +3141,7 @@ int mk_session_stack_push(mk_session *s, size_t inst, uint32_t stack, int32_t va
 int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *value)
 {
     if (!s || !value || inst >= s->n || stack >= (uint32_t)s->nstack) return MK_EINVAL;
+    if (s->native) return MK_EINVAL; // host-side state access: interpreter sessions (mixed networks) only
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     int32_t d = 0;
@@ -2932,6 +3156,7 @@ int mk_session_stack_pop(mk_session *s, size_t inst, uint32_t stack, int32_t *va
 int mk_session_input_take(mk_session *s, size_t inst, int32_t *value)
 {
     if (!s || !value || inst >= s->n) return MK_EINVAL;
+    if (s->native) return MK_EINVAL; // host-side state access: interpreter sessions (mixed networks) only
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     uint32_t io = 0;
@@ -2949,6 +3174,7 @@ int mk_session_input_take(mk_session *s, size_t inst, int32_t *value)
 int mk_session_output_put(mk_session *s, size_t inst, int32_t value)
 {
     if (!s || inst >= s->n) return MK_EINVAL;
+    if (s->native) return MK_EINVAL; // host-side state access: interpreter sessions (mixed networks) only
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     uint32_t io = 0;
@@ -2986,6 +3212,12 @@ int mk_session_cancel(mk_session *s)
                         args, 0, s->stream) != hipSuccess)
         return MK_EDEVICE;
     return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+}
+
+int mk_session_plan(const mk_session *s, char *out, size_t out_len)
+{
+    if (!s) return MK_EINVAL;
+    return mk::copy_out(out, out_len, s->plan);
 }
 
 void mk_session_free(mk_session *s) { delete s; }

@@ -439,6 +439,23 @@ int mkc_sess_lane(void *hv, uint32_t cap, uint32_t *nregs, uint32_t *nslots, cha
     return rc;
 }
 
+// The whole session module (lane + mk_sess_exec) as hiprtc gets it.
+int mkc_sess_module(void *hv, uint32_t cap, char *out, size_t out_len)
+{
+    auto *h = (CheckNet *)hv;
+    mk::SchedProgram P;
+    std::string w, src;
+    int rc = 0;
+    if (!mk::compile_session_schedule(h->net, cap, mk::SchedLimits{}, P, w) ||
+        !mk::jit_session_source(P, mk::JitLimits::from_env(), src, w)) {
+        src = w;
+        rc = 1;
+    }
+    if (src.size() + 1 > out_len) return -1;
+    memcpy(out, src.c_str(), src.size() + 1);
+    return rc;
+}
+
 // Lane function of the native tier (tis_jit.h) for the CPU tests: returns 0
 // with the source in `out`, 1 when the schedule or the JIT declined (why in
 // `out`), negative when `out` is too small.

@@ -315,6 +315,12 @@ class SessionSet:
             N.check(rc, what)
         return BatchResult(out, st, sp)
 
+    def plan(self) -> str:
+        """Which tier runs the sessions (mk_session_plan)."""
+        buf = C.create_string_buffer(1024)
+        N.check(N.lib().mk_session_plan(self._h, buf, len(buf)), "mk_session_plan")
+        return buf.value.decode()
+
     def cancel(self):
         """Abandon every instance's open call (mk_session_cancel)."""
         N.check(N.lib().mk_session_cancel(self._h), "mk_session_cancel")

@@ -190,3 +190,18 @@ def session_lane(nodes, *, stack_cap=None):
         return buf.value.decode(), nr.value, ns.value
     finally:
         lib().mkc_free(h)
+
+
+def session_module(nodes, *, stack_cap=None):
+    """The native session module's full source (what hiprtc compiles)."""
+    h, _keep = _load(nodes)
+    try:
+        lib().mkc_sess_module.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]
+        buf = C.create_string_buffer(1 << 24)
+        rc = lib().mkc_sess_module(h, 1024 if stack_cap is None else stack_cap, buf, len(buf))
+        if rc == 1:
+            raise NotCompiled(buf.value.decode())
+        assert rc == 0, rc
+        return buf.value.decode()
+    finally:
+        lib().mkc_free(h)

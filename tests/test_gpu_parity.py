@@ -754,3 +754,59 @@ def test_machine_input_order_is_transparent(gpu, monkeypatch, kind):
         out, st, sp, _ = res["1"]
         assert np.array_equal(out[-3000:], ref[0]) and np.array_equal(st[-3000:], ref[1]) and \
             np.array_equal(sp[-3000:], ref[2]), label
+
+
+# ---- native-tier sessions (tis_jit.h mk_sess_exec) ------
+# The session tests above run on the native tier whenever the network
+# compiles (a call that reaches its budget slice inside a superblock is
+# handed to the interpreter mid-call).  Here: which tier, both tiers against
+# each other and the oracle, and hand-offs inside bursts.
+
+def test_sessions_native_tier_plans(gpu):
+    for nodes in (mk.networks.example_network(), mk.networks.countdown_network(), mk.networks.sample_network(),
+                  mk.networks.pipeline_network(64)):
+        s = mk.Network(nodes).sessions(4)
+        assert s.plan().startswith("tier=native"), s.plan()
+        s.close()
+
+
+def test_sessions_interp_when_disabled(gpu, monkeypatch):
+    monkeypatch.setenv("MK_SESSION_NATIVE", "0")
+    s = mk.Network(mk.networks.example_network()).sessions(4)
+    assert s.plan().startswith("tier=interp reason=disabled"), s.plan()
+    r = s.compute([5, 6, 7, 8])
+    assert r.out.tolist() == [7, 8, 9, 10]
+
+
+@pytest.mark.parametrize("seed", range(0, 16))
+def test_sessions_native_handoff_bursts(gpu, seed):
+    # countdowns whose long calls cross the budget inside a burst: the native
+    # kernel answers the calls before the hand-off, the interpreter the rest
+    nodes = mk.networks.countdown_network() if seed % 2 == 0 else random_network(seed)
+    budget = [150, 400, 1000, 3000][seed % 4]
+    g, o = _session_pair(nodes, 256, budget=budget)
+    seqs = po.gen_inputs(seed * 5 + 1, 5 * 256, kind=1, mask=1023).reshape(5, 256)
+    got = g.compute_seq(seqs)
+    for k, row in enumerate(seqs):
+        assert_same(mk.network.BatchResult(got.out[k], got.status[k], got.steps[k]),
+                    o.compute(row, budget=budget, threads=THREADS), f"burst call {k}")
+    for j in range(3):
+        assert_same(g.resume(), o.resume(budget=budget, threads=THREADS), f"resume {j}")
+    g.cancel()
+    o.cancel()
+    row = po.gen_inputs(seed + 99, 256, kind=1, mask=1023)
+    assert_same(g.compute(row), o.compute(row, budget=budget, threads=THREADS), "after burst")
+
+
+def test_sessions_native_vs_interp_large(gpu, monkeypatch):
+    # the C2 network at 65,536 instances x 6 calls: native and interpreter agree
+    nodes = mk.networks.example_network()
+    xs = po.gen_inputs(SEED, 6 * 65536).reshape(6, 65536)
+    a = mk.Network(nodes).sessions(65536)
+    assert a.plan().startswith("tier=native")
+    monkeypatch.setenv("MK_SESSION_NATIVE", "0")
+    b = mk.Network(nodes).sessions(65536)
+    for row in xs:
+        ra, rb = a.compute(row), b.compute(row)
+        assert np.array_equal(ra.out, rb.out) and np.array_equal(ra.status, rb.status)
+        assert np.array_equal(ra.steps, rb.steps)

@@ -8,6 +8,8 @@ A call that would reach its budget slice inside a superblock is handed off
 interpreter's terms (sess_convert.h) and the oracle, importing it, must
 finish that call and every later one exactly as the oracle's own run does.
 CPU only."""
+import os
+
 import numpy as np
 import pytest
 
@@ -224,3 +226,21 @@ def test_generated_session_lane(tmp_path):
             for a, r in zip((out, st, sp), ref):
                 bad = np.nonzero(a != r)[0]
                 assert not bad.size, (label, k, int(bad[0]), int(a[bad[0]]), int(r[bad[0]]))
+
+
+def test_session_modules_compile_for_gfx950(tmp_path):
+    # the whole module (lane + mk_sess_exec) through this ROCm's hiprtc, as
+    # the loader compiles it (mk_rtc; no GPU needed)
+    import subprocess
+
+    import schedcheck as sc
+
+    rtc = os.path.join(os.path.dirname(mk._native.LIB_PATH), "mk_rtc")
+    for name, nodes in [("example", mk.networks.example_network()), ("countdown", mk.networks.countdown_network()),
+                        ("pipeline64", mk.networks.pipeline_network(64)), ("rand3", random_network(3))]:
+        src = sc.session_module(nodes)
+        p = tmp_path / f"{name}.hip"
+        p.write_text(src)
+        r = subprocess.run([rtc, str(p), str(tmp_path / f"{name}.co")], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (name, r.stdout[-2000:])
+        assert (tmp_path / f"{name}.co").stat().st_size > 0
