@@ -67,7 +67,7 @@ namespace mk {
 constexpr int kBlock = 256;
 // Native sessions' markers (tis_jit.cpp MK_SS_*; 0xFFFFFFF0 = ended): held by
 // the interpreter, handed off in this launch.
-constexpr uint32_t kSessT1 = 0xFFFFFFF1u, kSessHand = 0xFFFFFFF2u;
+constexpr uint32_t kSessDead = 0xFFFFFFF0u, kSessT1 = 0xFFFFFFF1u, kSessHand = 0xFFFFFFF2u;
 constexpr int kMaxDevices = 64;
 
 struct KParams {
@@ -1233,6 +1233,14 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
                 p.csteps[gid] = steps;
             }
         }
+    } else if (gid < n && p.nsb && p.resume) {
+        // a resume launch runs only this kernel: sessions the native tier
+        // holds never have a call open (a budget slice hands the call to this
+        // kernel), so there is nothing to resume -- or the session ended
+        // (tis_oracle.c session_step)
+        p.out[ci] = 0;
+        p.status[ci] = p.nsb[gid] == kSessDead ? (uint8_t)MK_ST_STACK_OVERFLOW : (uint8_t)0;
+        if (p.steps) p.steps[ci] = 0u;
     }
     } // calls
 
@@ -1682,7 +1690,7 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
     if (!jit_slots_in_lds(P.nslots, true, lim)) return 0;
     // LDS allocation granule: measured, 207 slots (52,992 B) fit three waves per
     // CU and 212 (54,272 B) do not (r02af), so a 2 KiB granule is assumed
-    const uint64_t bytes = ((uint64_t)P.nslots * 256u + 2047u) / 2048u * 2048u;
+    const uint64_t bytes = ((uint64_t)jit_lds_words(P.nslots) * 256u + 2047u) / 2048u * 2048u;
     return std::min<uint32_t>(4u, (uint32_t)((160u * 1024u) / bytes));
 }
 
@@ -1721,7 +1729,7 @@ bool heavy_stream(const SchedProgram &P, const JitLimits &jl)
 void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
-    auto bytes = [](uint32_t n) { return ((uint64_t)n * 256u + 2047u) / 2048u * 2048u; };
+    auto bytes = [](uint32_t n) { return ((uint64_t)jit_lds_words(n) * 256u + 2047u) / 2048u * 2048u; };
     if (!heavy_stream(sc->prog, jl)) return;
     if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) return; // the knob's budget holds them
     SchedProgram best = sc->prog;
@@ -2247,9 +2255,13 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
     J.src_bytes = src.size();
     J.src_hash = src_hash(src);
     if (!rtc_compile(src, lim.max_compile_s, J.code, J.why, J.rtc)) return false;
-    if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded
-        if (FILE *f = std::fopen(d, "wb")) {
+    if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded,
+        if (FILE *f = std::fopen(d, "wb")) {                   // and its source beside it (<path>.hip)
             std::fwrite(J.code.data(), 1, J.code.size(), f);
+            std::fclose(f);
+        }
+        if (FILE *f = std::fopen((std::string(d) + ".hip").c_str(), "wb")) {
+            std::fwrite(src.data(), 1, src.size(), f);
             std::fclose(f);
         }
     }

@@ -967,6 +967,12 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
 void emit_lds_access(Emitter &e, const JitLimits &lim)
 {
     e.line("#define MK_LDS_SLOTS %s", lim.lds_volatile ? "((volatile int32_t *)mk_lds_slots)" : "mk_lds_slots");
+    // word of slot s of this lane (JitLimits::lds_quad); the array holds
+    // whole quads: ceil(slots / 4) * 4 * 64 words
+    if (lim.lds_quad)
+        e.line("#define MK_LDS_IX(s) ((((uint32_t)(s) >> 2) * 64u + (threadIdx.x & 63u)) * 4u + ((uint32_t)(s) & 3u))");
+    else
+        e.line("#define MK_LDS_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
 }
 
 void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps, bool checked)
@@ -991,7 +997,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOTS_BUFFER 1");
         e.line("#define MK_SLOTS_LDS_N %uu", nl);
         e.line("#define MK_HBM_NSLOTS (MK_NSLOTS - MK_SLOTS_LDS_N)");
-        e.line("__shared__ int32_t mk_lds_slots[MK_SLOTS_LDS_N * 64u];");
+        e.line("__shared__ int32_t mk_lds_slots[((MK_SLOTS_LDS_N + 3u) & ~3u) * 64u];");
         emit_lds_access(e, *g.lim);
         e.line("MK_FN __amdgpu_buffer_rsrc_t mk_slot_rsrc(int32_t *b)");
         e.line("{");
@@ -1000,12 +1006,12 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOT_LANE ((int32_t)((threadIdx.x & 63u) * 4u))");
         e.line("MK_FN void mk_slot_st(int32_t *b, uint32_t s, int32_t v)");
         e.line("{");
-        e.line("    if (s < MK_SLOTS_LDS_N) MK_LDS_SLOTS[s * 64u + (threadIdx.x & 63u)] = v;");
+        e.line("    if (s < MK_SLOTS_LDS_N) MK_LDS_SLOTS[MK_LDS_IX(s)] = v;");
         e.line("    else __builtin_amdgcn_raw_buffer_store_b32(v, mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
         e.line("}");
         e.line("MK_FN int32_t mk_slot_ld(int32_t *b, uint32_t s)");
         e.line("{");
-        e.line("    if (s < MK_SLOTS_LDS_N) return MK_LDS_SLOTS[s * 64u + (threadIdx.x & 63u)];");
+        e.line("    if (s < MK_SLOTS_LDS_N) return MK_LDS_SLOTS[MK_LDS_IX(s)];");
         e.line("    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(mk_slot_rsrc(b), (int32_t)((uint32_t)MK_SLOT_LANE + (s - MK_SLOTS_LDS_N) * 256u), 0, 0);");
         e.line("}");
         e.line("#undef MK_SLOT_ST");
@@ -1019,13 +1025,14 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#endif");
     } else if (nl) {
         // Heavy kernel, slots in LDS: one wave per block owns nslots x 64
-        // words, slot s of lane l at word s * 64 + l (a wave's access is 64
-        // consecutive words: conflict-free).  No HBM traffic for the stacks.
+        // words, slot s of lane l at MK_LDS_IX(s) (a wave's access is 64
+        // consecutive words, or 64 consecutive 16-byte quads: conflict-free).
+        // No HBM traffic for the stacks.
         e.line("#ifndef MK_LANE_CHECKED");
         e.line("#define MK_SLOTS_LDS 1");
-        e.line("__shared__ int32_t mk_lds_slots[MK_NSLOTS * 64u];");
+        e.line("__shared__ int32_t mk_lds_slots[((MK_NSLOTS + 3u) & ~3u) * 64u];");
         emit_lds_access(e, *g.lim);
-        e.line("#define MK_SLOT_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
+        e.line("#define MK_SLOT_IX(s) MK_LDS_IX(s)");
         e.line("#undef MK_SLOT_ST");
         e.line("#undef MK_SLOT_LD");
         e.line("#undef MK_SLOT_STX");
@@ -1637,7 +1644,7 @@ bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
 {
     // one workgroup may hold at most the CU's 160 KiB of LDS
     const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
-    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt && (uint64_t)nslots * 256u <= cap;
+    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt && (uint64_t)jit_lds_words(nslots) * 256u <= cap;
 }
 
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
@@ -2089,6 +2096,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_LDS_SPLIT", l.lds_split);
     flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
     flag("MK_JIT_NARROW", l.narrow);
+    flag("MK_JIT_LDS_QUAD", l.lds_quad);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2098,12 +2106,12 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)ts_dyn,
              (int)tune_regs,
-             lds_split, (int)lds_volatile, (int)narrow);
+             lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad);
     return b;
 }
 
@@ -2438,7 +2446,9 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool)
     e.line("MK_FN int32_t mk_flag_gt(int32_t x) { int32_t f; __asm__(\"v_med3_i32 %%0, %%1, 0, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
     e.line("MK_FN int32_t mk_flag_lt(int32_t x) { int32_t f; __asm__(\"v_lshrrev_b32 %%0, 31, %%1\" : \"=v\"(f) : \"v\"(x)); return f; }");
     e.line("MK_FN int32_t mk_flag_nz(int32_t x) { int32_t f; __asm__(\"v_min_u32 %%0, 1, %%1\" : \"=v\"(f) : \"v\"(x)); return f; }");
-    e.line("MK_FN int32_t mk_flag_min(int32_t x, int32_t g) { int32_t f; __asm__(\"v_min_u32 %%0, %%1, %%2\" : \"=v\"(f) : \"v\"(x), \"v\"(g)); return f; }");
+    // (the min stays v_min_u32 in plain C; inline asm would cost an s_nop
+    // after every one -- the hazard recognizer cannot see into asm)
+    e.line("MK_FN int32_t mk_flag_min(int32_t x, int32_t g) { return (int32_t)((uint32_t)x < (uint32_t)g ? (uint32_t)x : (uint32_t)g); }");
     e.line("MK_FN int32_t mk_mad24(int32_t f, int32_t k, int32_t x)");
     e.line("{");
     e.line("    int32_t r;");

@@ -1574,6 +1574,10 @@ SchedLimits lim_env(SchedLimits lim)
     if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_SIDE_EXITS")) lim.side_exits = atoi(e) != 0;
     if (const char *e = getenv("MK_SCHED_SHARE")) lim.share_slots = atoi(e) != 0;
+    if (const char *e = getenv("MK_SCHED_MAX_REGS")) {
+        const int v = atoi(e);
+        if (v >= 8 && v <= 1024) lim.max_regs = (uint32_t)v;
+    }
     if (const char *e = getenv("MK_SCHED_SOFT_REGS")) {
         const int v = atoi(e);
         if (v >= 4 && (uint32_t)v < lim.max_regs) lim.soft_regs = (uint32_t)v;

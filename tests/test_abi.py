@@ -92,6 +92,52 @@ def test_c_client_load_errors_and_no_gpu(tmp_path):
         assert r.returncode == 3 and r.stdout == "compute -4\n"
 
 
+def _build_c_bench(tmp_path):
+    """integration/c/mk_bench.c: the batched path timed through the ABI alone
+    (no PyTorch in the process), HIP runtime for buffers and events."""
+    import subprocess
+
+    lib = os.path.dirname(mk._native.LIB_PATH)
+    exe = str(tmp_path / "mk_bench")
+    subprocess.check_call(["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                           os.path.join(ROOT, "integration", "c", "mk_bench.c"), "-L", lib, "-lmisaka_amd",
+                           "-L", "/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib",
+                           "-o", exe])
+    return exe
+
+
+@pytest.mark.parametrize("depth", [64, 256, 1024])
+def test_c_bench_networks_match_bench_py(tmp_path, depth):
+    # the C timing client runs bench.py's networks: same program text
+    import subprocess
+
+    exe = _build_c_bench(tmp_path)
+    r = subprocess.run([exe, f"c4:{depth}", "print"], capture_output=True, text=True, check=True)
+    got = {}
+    for block in r.stdout.split("== ")[1:]:
+        head, _, text = block.partition("\n")
+        name, kind = head.split()
+        got[name] = (int(kind), text)
+    want = {n.name: ({"program": 0, "stack": 1}[n.kind], n.program if n.kind == "program" else "")
+            for n in mk.networks.pipeline_network(depth)}
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl", ["c2", "c4:64"])
+def test_c_bench_on_gpu(gpu, tmp_path, wl):
+    import json
+    import subprocess
+
+    exe = _build_c_bench(tmp_path)
+    r = subprocess.run([exe, wl, "3", "1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["plan"].startswith("tier=native") and "rtc=linked" in rec["plan"], rec["plan"]
+    assert rec["node_instr_per_s"] > 0 and rec["results_per_launch"] == rec["lanes"]
+
+
 @pytest.mark.gpu
 def test_c_client_compute_on_gpu(gpu, tmp_path):
     import subprocess
