@@ -202,10 +202,21 @@ int mk_session_compute(mk_session *s, const int64_t *in, int32_t *out, uint8_t *
 int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int32_t *out, uint8_t *status,
                            uint32_t *steps);
 
-/* The same on device arrays, asynchronous on `stream` (NULL = the session's
- * own stream); calls on one session are ordered. */
+/* One call on device arrays, asynchronous on `stream` (NULL = the session's
+ * own stream); calls on one session are ordered (device-side: a caller stream
+ * and the session's stream wait for each other through an event, no host
+ * synchronisation). */
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
                               uint32_t *d_steps, void *stream);
+
+/* mk_session_compute_seq on device arrays ([call][session], d_steps
+ * nullable), asynchronous on `stream` like mk_session_compute_device: a burst
+ * of ncalls sequential /compute calls per instance in one launch, the state
+ * loaded from HBM once and stored once.  Statuses report MK_ST_CALL_OPEN as
+ * the host call does; nothing here returns MK_EBUSY (the statuses stay on the
+ * device). */
+int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t ncalls, int32_t *d_out,
+                                  uint8_t *d_status, uint32_t *d_steps, void *stream);
 
 /* ---- mixed deployments (row f4): sessions of a network with remote peers --
  * A call on such a session runs until it has its output or nothing more can

@@ -121,6 +121,8 @@ SIGNATURES = {
     "mk_session_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_compute_seq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_compute_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mk_session_compute_seq_device": (
+        C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mk_session_reset": (C.c_int, [C.c_void_p]),
     "mk_session_cancel": (C.c_int, [C.c_void_p]),
     "mk_session_plan": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),

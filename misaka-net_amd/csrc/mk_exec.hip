@@ -965,6 +965,10 @@ struct SessParams {
     // round position io bits 9-13 with io bit 14 "something changed".
     const uint32_t *nsb;       // [n]
     const uint32_t *hand_call; // [n]
+    // [0] launch epoch of the last hand-off, [1] sessions the interpreter
+    // holds (tis_session_import counts them): with none and no resume this
+    // kernel has nothing to do
+    const uint32_t *sflags;
 };
 
 template <int NMAX>
@@ -977,6 +981,7 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     const uint64_t n = p.n;
     int32_t *const port = lds;                     // [nprog*4][B]
     int32_t *const sdepth = lds + p.nprog * 4 * B; // [nstack][B]
+    if (p.nsb && !p.resume && p.sflags[1] == 0u) return; // every session is the native tier's
     const bool live = gid < n && (!p.nsb || p.nsb[gid] == kSessT1);
 
     int64_t acc[NMAX], bak[NMAX];
@@ -1287,6 +1292,8 @@ struct SessImport {
     uint64_t n;
     int nprog, nstack;
     uint32_t *nsb;
+    uint32_t *sflags;   // SessParams::sflags (written here)
+    uint32_t epoch;     // this launch (the native kernel stores it into sflags[0] at a hand-off)
     const uint32_t *hand_sb, *hand_steps;
     const int64_t *regs;  // [register][n]
     const int32_t *slots; // [slot][n]
@@ -1323,6 +1330,7 @@ struct SessImportOut {
 
 __global__ void __launch_bounds__(kBlock) tis_session_import(SessImport q, SessParams p)
 {
+    if (q.sflags[0] != q.epoch) return; // nothing was handed off in this launch
     const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (gid >= q.n || q.nsb[gid] != kSessHand) return;
     const SessMapHdr h = q.hdr[q.hand_sb[gid]];
@@ -1334,6 +1342,7 @@ __global__ void __launch_bounds__(kBlock) tis_session_import(SessImport q, SessP
     p.io[gid] = o.io;
     p.csteps[gid] = q.hand_steps[gid];
     q.nsb[gid] = kSessT1;
+    atomicAdd(&q.sflags[1], 1u);
 }
 
 // ---- input order for the machine shape (tier 3) -----------------------------
@@ -2554,6 +2563,9 @@ struct mk_session {
     void *d_native = nullptr; // every native array, one allocation
     size_t native_bytes = 0;
     uint32_t *nsb = nullptr, *hand_sb = nullptr, *hand_steps = nullptr, *hand_call = nullptr;
+    uint32_t *sflags = nullptr; // SessParams::sflags
+    uint32_t epoch = 0;         // native launches so far (never 0 after the first)
+    hipEvent_t order = nullptr; // orders caller streams against the session's stream
     int64_t *regs = nullptr;
     int32_t *slots = nullptr;
     mk::SessMapHdr *hdr = nullptr;
@@ -2568,6 +2580,7 @@ struct mk_session {
         (void)hipFree(d_stage);
         (void)hipHostFree(h_stage);
         if (mod) (void)hipModuleUnload(mod);
+        if (order) (void)hipEventDestroy(order);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -2587,6 +2600,8 @@ struct SessK {
     int64_t *regs;
     int32_t *slots;
     uint32_t *hand_sb, *hand_steps, *hand_call;
+    uint32_t *sflags;
+    uint32_t epoch;
 };
 
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
@@ -2605,16 +2620,17 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
     const uint64_t blocks = (s->n + kBlock - 1) / kBlock;
     if (blocks > 0x7fffffffull) return MK_ELIMIT;
     if (s->native && !resume) {
+        if (++s->epoch == 0) s->epoch = 1; // sflags[0] starts at 0: "no hand-off yet"
         // 1. the native kernel: every session it holds, every call of the burst
         SessK k{s->n, ncalls, p.budget, d_in, d_out, d_status, d_steps, s->nsb, s->regs, s->slots,
-                s->hand_sb, s->hand_steps, s->hand_call};
+                s->hand_sb, s->hand_steps, s->hand_call, s->sflags, s->epoch};
         void *kargs[] = {(void *)&k};
         if (hipModuleLaunchKernel(s->fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr) !=
             hipSuccess)
             return MK_EDEVICE;
         // 2. calls it handed off become interpreter sessions
-        SessImport q{s->n, s->nprog, s->nstack, s->nsb, s->hand_sb, s->hand_steps, s->regs, s->slots,
-                     s->hdr, s->rec, s->dyn_base};
+        SessImport q{s->n, s->nprog, s->nstack, s->nsb, s->sflags, s->epoch, s->hand_sb, s->hand_steps, s->regs,
+                     s->slots, s->hdr, s->rec, s->dyn_base};
         void *iargs[] = {(void *)&q, (void *)&p};
         if (hipLaunchKernel(reinterpret_cast<void *>(&tis_session_import), dim3((unsigned)blocks), dim3(kBlock), iargs,
                             0, stream) != hipSuccess)
@@ -2666,7 +2682,7 @@ int session_native(mk_session *s)
     const size_t N = s->n ? s->n : 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t sz[] = {al(N * 4), al((size_t)P.nregs * N * 8), al((size_t)std::max<uint32_t>(P.nslots, 1) * N * 4),
-                         al(N * 4), al(N * 4), al(N * 4), al(hdr.size() * sizeof(SessMapHdr)),
+                         al(N * 4), al(N * 4), al(N * 4), al(16), al(hdr.size() * sizeof(SessMapHdr)),
                          al(rec.size() * sizeof(SessSrcDev)), al(std::max<size_t>(P.dyn_base.size(), 1) * 8)};
     size_t total = 0;
     for (size_t b : sz) total += b;
@@ -2681,9 +2697,10 @@ int session_native(mk_session *s)
     s->hand_sb = (uint32_t *)take(3);
     s->hand_steps = (uint32_t *)take(4);
     s->hand_call = (uint32_t *)take(5);
-    s->hdr = (SessMapHdr *)take(6);
-    s->rec = (SessSrcDev *)take(7);
-    s->dyn_base = (int64_t *)take(8);
+    s->sflags = (uint32_t *)take(6);
+    s->hdr = (SessMapHdr *)take(7);
+    s->rec = (SessSrcDev *)take(8);
+    s->dyn_base = (int64_t *)take(9);
     // the maps never change: copied once (reset clears only the lane state)
     if ((!hdr.empty() && hipMemcpy(s->hdr, hdr.data(), hdr.size() * sizeof(SessMapHdr), hipMemcpyHostToDevice) !=
                              hipSuccess) ||
@@ -2692,10 +2709,11 @@ int session_native(mk_session *s)
         (!P.dyn_base.empty() &&
          hipMemcpy(s->dyn_base, P.dyn_base.data(), P.dyn_base.size() * 8, hipMemcpyHostToDevice) != hipSuccess))
         return MK_EDEVICE;
-    s->native_bytes = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5]; // the lane state: what a reset clears
+    s->native_bytes = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5] + sz[6]; // the lane state: what a reset clears
     s->native = true;
     s->p.nsb = s->nsb;
     s->p.hand_call = s->hand_call;
+    s->p.sflags = s->sflags;
     char line[256];
     snprintf(line, sizeof line, "tier=native superblocks=%u regs=%u slots=%u words=%zu source=%zuB kernel=%016llx "
              "compile=%.2fs rtc=%s", P.nsb, P.nregs, P.nslots, P.code.size(), src.size(),
@@ -2958,25 +2976,34 @@ int mk_session_reset(mk_session *s)
     return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 
-int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
-                              uint32_t *d_steps, void *stream)
+int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t ncalls, int32_t *d_out,
+                                  uint8_t *d_status, uint32_t *d_steps, void *stream)
 {
-    if (!s || (s->n && (!d_in || !d_out || !d_status))) return MK_EINVAL;
+    if (!s || (s->n && ncalls && (!d_in || !d_out || !d_status))) return MK_EINVAL;
+    if (ncalls > 0xffffffffull) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    // the session state is ordered on the session's own stream
-    if (stream && hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
-    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st);
-    if (rc) return rc;
+    // the session state is ordered on the session's own stream: a caller
+    // stream waits for it (device-side, no host synchronisation), and it for
+    // the caller stream's launches
     if (stream) {
-        hipEvent_t ev;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
-        (void)hipEventRecord(ev, st);
-        (void)hipStreamWaitEvent(s->stream, ev, 0);
-        (void)hipEventDestroy(ev);
+        if (!s->order && hipEventCreateWithFlags(&s->order, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
+        if (hipEventRecord(s->order, s->stream) != hipSuccess || hipStreamWaitEvent(st, s->order, 0) != hipSuccess)
+            return MK_EDEVICE;
     }
+    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls);
+    if (rc) return rc;
+    if (stream &&
+        (hipEventRecord(s->order, st) != hipSuccess || hipStreamWaitEvent(s->stream, s->order, 0) != hipSuccess))
+        return MK_EDEVICE;
     return MK_OK;
+}
+
+int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
+                              uint32_t *d_steps, void *stream)
+{
+    return mk_session_compute_seq_device(s, d_in, 1, d_out, d_status, d_steps, stream);
 }
 
 extern "C++" {

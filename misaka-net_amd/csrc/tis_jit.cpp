@@ -2525,6 +2525,8 @@ struct SessK {
     uint32_t *hand_sb;   // [n] superblock of a hand-off
     uint32_t *hand_steps;// [n] the call's steps at it
     uint32_t *hand_call; // [n] the call of the burst it happened in
+    uint32_t *sflags;    // [0]: this launch's epoch once a lane handed off (mk_exec.hip SessParams)
+    uint32_t epoch;
 };
 extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
 {
@@ -2556,6 +2558,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
             p.hand_sb[gid] = L.next / 2u;
             p.hand_steps[gid] = L.steps;
             p.hand_call[gid] = call;
+            p.sflags[0] = p.epoch; // the import kernel has work
             sbv = MK_SS_HAND;
             continue;
         }

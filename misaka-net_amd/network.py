@@ -8,7 +8,9 @@ loaded ``mk_net`` handle.  ``compute_batch`` evaluates many independent
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import Iterable, Mapping, Optional, Sequence
 
@@ -22,6 +24,23 @@ STATUS_NAMES = {
     N.MK_ST_STACK_OVERFLOW: "stack_overflow",
     N.MK_ST_OUTPUT_STOP: "output_stop",
 }
+
+
+# Native handles still open at interpreter exit are freed by an atexit hook
+# (sessions before the networks they run on), while the HIP runtime and the
+# caller's GPU state are intact, instead of by garbage collection during
+# teardown or never.
+_LIVE: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live():
+    live = list(_LIVE)
+    for o in [o for o in live if isinstance(o, SessionSet)] + [o for o in live if isinstance(o, Network)]:
+        try:
+            o.close()
+        except Exception:  # pragma: no cover - best effort at exit
+            pass
 
 
 class TisParseError(ValueError):
@@ -115,6 +134,7 @@ class Network:
         N.check(rc, err.value.decode(errors="surrogateescape"))
         self._h = h
         self.specs = specs
+        _LIVE.add(self)
 
     @classmethod
     def from_node_info(cls, node_info: Mapping[str, Mapping], programs: Mapping[str, str], master: Optional[str] = None):
@@ -287,6 +307,7 @@ class SessionSet:
         h = C.c_void_p()
         N.check(N.lib().mk_session_create(net.handle, device, n, C.byref(o), C.byref(h)), "mk_session_create")
         self._h, self._net, self.n, self.device = h, net, n, device
+        _LIVE.add(self)
 
     def compute(self, values, *, steps=True, busy_ok=False) -> BatchResult:
         """One /compute call per instance: ``values[i]`` goes to instance i.
@@ -352,6 +373,12 @@ class SessionSet:
     def compute_device(self, in_ptr, out_ptr, status_ptr, steps_ptr=None, *, stream=None):
         N.check(N.lib().mk_session_compute_device(self._h, in_ptr, out_ptr, status_ptr, steps_ptr, stream),
                 "mk_session_compute_device")
+
+    def compute_seq_device(self, in_ptr, ncalls, out_ptr, status_ptr, steps_ptr=None, *, stream=None):
+        """A burst of `ncalls` sequential calls per instance in one launch on
+        device arrays laid out [call][instance] (mk_session_compute_seq_device)."""
+        N.check(N.lib().mk_session_compute_seq_device(self._h, in_ptr, ncalls, out_ptr, status_ptr, steps_ptr, stream),
+                "mk_session_compute_seq_device")
 
     def reset(self):
         """/reset (master.go:126-143): every instance back to its initial state."""

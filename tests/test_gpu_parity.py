@@ -810,3 +810,40 @@ def test_sessions_native_vs_interp_large(gpu, monkeypatch):
         ra, rb = a.compute(row), b.compute(row)
         assert np.array_equal(ra.out, rb.out) and np.array_equal(ra.status, rb.status)
         assert np.array_equal(ra.steps, rb.steps)
+
+
+# Device-array session APIs (mk_session_compute_device on a caller stream,
+# mk_session_compute_seq_device bursts; bench.py's sessions leg) against the
+# oracle's sessions: the same calls in the same order, one launch per call or
+# one launch per burst, with budget slices that hand calls off mid-burst.
+@pytest.mark.parametrize("seed", [0, 3, 7, 12])
+def test_session_device_bursts_match_oracle(gpu, seed):
+    import torch
+
+    nodes = mk.networks.example_network() if seed == 0 else random_network(seed)
+    n, calls = 1000, 5
+    budget = None if seed == 0 else [300, 1000, 5000][seed % 3]
+    xs = po.gen_inputs(seed * 31 + 7, calls * n, kind=0 if seed == 0 else 1, mask=1023).reshape(calls, n)
+    o = po.OracleSessions(po.OracleNet(nodes), n)
+    refs = [o.compute(row, budget=budget, threads=THREADS) for row in xs]
+    s = torch.cuda.Stream()
+    x = torch.from_numpy(xs).cuda()
+    for burst in (False, True):
+        g = mk.Network(nodes).sessions(n, budget=budget)
+        out = torch.empty((calls, n), dtype=torch.int32, device="cuda")
+        st = torch.empty((calls, n), dtype=torch.uint8, device="cuda")
+        sp = torch.empty((calls, n), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        if burst:
+            g.compute_seq_device(x.data_ptr(), calls, out.data_ptr(), st.data_ptr(), sp.data_ptr(),
+                                 stream=s.cuda_stream)
+        else:
+            for c in range(calls):
+                g.compute_device(x[c].data_ptr(), out[c].data_ptr(), st[c].data_ptr(), sp[c].data_ptr(),
+                                 stream=s.cuda_stream)
+        s.synchronize()
+        for c in range(calls):
+            got = mk.network.BatchResult(out[c].cpu().numpy(), st[c].cpu().numpy(),
+                                         sp[c].cpu().numpy().astype(np.uint32))
+            assert_same(got, refs[c], f"burst={burst} call {c}")
+        g.close()
