@@ -1699,7 +1699,7 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
     if (!jit_slots_in_lds(P.nslots, true, lim)) return 0;
     // LDS allocation granule: measured, 207 slots (52,992 B) fit three waves per
     // CU and 212 (54,272 B) do not (r02af), so a 2 KiB granule is assumed
-    const uint64_t bytes = ((uint64_t)jit_lds_words(P.nslots) * 256u + 2047u) / 2048u * 2048u;
+    const uint64_t bytes = ((uint64_t)jit_lds_words(P.nslots, lim.lds_quad) * 256u + 2047u) / 2048u * 2048u;
     return std::min<uint32_t>(4u, (uint32_t)((160u * 1024u) / bytes));
 }
 
@@ -1738,7 +1738,7 @@ bool heavy_stream(const SchedProgram &P, const JitLimits &jl)
 void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
-    auto bytes = [](uint32_t n) { return ((uint64_t)jit_lds_words(n) * 256u + 2047u) / 2048u * 2048u; };
+    auto bytes = [&](uint32_t n) { return ((uint64_t)jit_lds_words(n, jl.lds_quad) * 256u + 2047u) / 2048u * 2048u; };
     if (!heavy_stream(sc->prog, jl)) return;
     if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) return; // the knob's budget holds them
     SchedProgram best = sc->prog;

@@ -140,8 +140,9 @@ struct JitLimits {
     // word ((s / 4) * 64 + l) * 4 + s % 4, so four consecutive slots of a lane
     // are one 16-byte word and LLVM merges a stack's consecutive pushes and
     // pops into ds_write_b128 / ds_read_b128 (twice the LDS bytes per clock of
-    // b32 accesses).  Off: slot s at s * 64 + l.
-    bool lds_quad = true;
+    // b32 accesses).  Off (default): slot s at s * 64 + l.  Measured r03f:
+    // C4 D=64 47.6 us with quads vs 24.2 without, D=256 159.5 vs 161.8.
+    bool lds_quad = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
@@ -172,7 +173,7 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
 // Whether the heavy stream kernel keeps the lane's `nslots` stack slots in
 // LDS (the executor then allocates no HBM slots and launches one grid).
 // LDS words per lane for n slots: whole quads (JitLimits::lds_quad)
-inline uint32_t jit_lds_words(uint32_t n) { return (n + 3u) & ~3u; }
+inline uint32_t jit_lds_words(uint32_t n, bool quad) { return quad ? (n + 3u) & ~3u : n; }
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim);
 // Slots of the lane the heavy stream kernel keeps in LDS: all (jit_slots_in_lds),
 // the first ones with JitLimits::lds_split, or none.
