@@ -2560,6 +2560,7 @@ struct mk_session {
     std::string plan; // mk_session_plan
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    std::vector<char> code; // the module's code object: HIP may read the image after hipModuleLoadData
     void *d_native = nullptr; // every native array, one allocation
     size_t native_bytes = 0;
     uint32_t *nsb = nullptr, *hand_sb = nullptr, *hand_steps = nullptr, *hand_call = nullptr;
@@ -2669,7 +2670,7 @@ int session_native(mk_session *s)
     }
     if (src.size() > h->jit_lim.max_src_bytes) return decline("session source over the native tier's size bound");
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<char> code;
+    std::vector<char> &code = s->code; // kept while the module is loaded
     if (!rtc_compile(src, h->jit_lim.max_compile_s, code, why, from)) return decline(why);
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     DeviceGuard g(s->device);

@@ -7,7 +7,11 @@ are compile / warm-up launches and are skipped):
   * HBM bytes: FETCH_SIZE and WRITE_SIZE (KiB, summed over the XCD rows) from
     separate passes.  gfx950 correction (MI355X_MICROARCH.md section HBM):
     FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so it
-    is doubled; WRITE_SIZE is taken as is.  These are L2 <-> fabric bytes
+    is doubled; WRITE_SIZE is taken as is.  Calibrated for the stack slots'
+    own pattern too (tools/probe/pmc_calib.hip, profiles/r03g_pmc_calib.json:
+    4 GiB moved by wave-blocked 4-byte buffer loads read FETCH_SIZE = 0.500x,
+    the 16-byte streaming loads 0.500x, 4-byte buffer stores WRITE_SIZE =
+    1.000x), so one factor serves every workload here.  These are L2 <-> fabric bytes
     (Infinity-Cache hits included), i.e. what left the XCDs' L2s.
   * SQ counters (one pass of 8 SQ + GRBM_GUI_ACTIVE): VALU / SALU wave-
     instructions, VALU lane cycles, waves, vector memory instructions.
@@ -67,7 +71,8 @@ for cfg in cfgs:
         "executor": rec["config"]["executor"],
         "fetch_kib_raw": fetch["FETCH_SIZE"],
         "write_kib_raw": write["WRITE_SIZE"],
-        "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 wide streaming reads); write bytes = WRITE_SIZE x 1024",
+        "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950; calibrated for 16-byte streaming and 4-byte "
+                      "buffer loads, profiles/r03g_pmc_calib.json); write bytes = WRITE_SIZE x 1024 (4-byte stores 1.000x)",
         "hbm_bytes_per_launch": hbm,
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": hbm / alg,
