@@ -3419,7 +3419,15 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                                     : "",
                  sc->jit.src_bytes, (unsigned long long)sc->jit.src_hash,
                  sc->jit.code.size(), sc->jit.compile_s, sc->jit.rtc.c_str());
-        s = std::string("tier=native ") + buf + tail + " knobs=" + h->jit_lim.key();
+        s = std::string("tier=native ") + buf + tail;
+        // heavy kernel, slots in HBM: at most this many inputs per launch
+        // (the slot memory cap, JitLimits::slot_bytes; launch_jit_locked)
+        const uint32_t hbm_slots = P.nslots - sc->jit.lds_n;
+        if (sc->jit.shape == mk::JIT_STREAM && sc->jit.heavy && hbm_slots) {
+            const uint64_t blk = (uint64_t)sc->jit.block, fit = h->jit_lim.slot_bytes / ((uint64_t)hbm_slots * 4u);
+            s += " chunk=" + std::to_string(std::max<uint64_t>(blk, fit / blk * blk));
+        }
+        s += " knobs=" + h->jit_lim.key();
     } else {
         const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
         uint32_t B, K;

@@ -27,7 +27,11 @@ enum JitShape { JIT_STREAM = 0, JIT_MACHINE = 1 };
 constexpr size_t kJitHeavyOps = 256; // stream lanes above this size: one lane per thread
 // Heavy kernels run one thread per input; a launch covers at most as many
 // inputs as fit this much stack-slot memory (more take several launches).
-constexpr size_t kJitSlotBytes = size_t(16) << 30;
+// 256 MiB: a launch's slot blocks stay in the 256 MB Infinity Cache, so the
+// pushes and pops of a launch mostly never reach HBM (r03g/r03h, C4 D=1024
+// at 256K lanes: 2.72 ms in one launch of 1 GB of slots; 2.30-2.43 ms in
+// launches of 128-256 MiB, 2.55 at 320, 4.0 at 48 -- too few waves).
+constexpr size_t kJitSlotBytes = size_t(256) << 20;
 // Heavy stream kernel: stack slots in LDS up to this many bytes per wave
 // (JitLimits::lds_slot_bytes): two waves per CU.  Measured on MI355X (r02x,
 // r02an): C4 D=64 (41 shared slots, 10 KB per wave) 194 -> 59 us against its

@@ -63,12 +63,21 @@ for cfg in cfgs:
     lanes = rec["config"]["lanes_per_gpu"]
     retired = rec["node_instr_per_lane"] * lanes
     alg = rec["roofline_hbm"]["bytes_per_launch"]
+    # a heavy kernel with HBM slots takes ceil(lanes / chunk) dispatches per
+    # step (mk_net_plan's chunk=); the counters above are per dispatch
+    plan = dict(w.split("=", 1) for w in rec["config"]["executor"].split() if "=" in w)
+    per_step = -(-lanes // int(plan["chunk"])) if "chunk" in plan else 1
+    for d in (fetch, write, sq, lds):
+        for k in list(d):
+            if not k.endswith("_dispatches"):
+                d[k] *= per_step
     hbm = int(2 * fetch["FETCH_SIZE"] * 1024 + write["WRITE_SIZE"] * 1024)
     out = {
         "workload": workload,
         "source": f"gpurun_out/{tag}/{cfg} (rocprofv3 --kernel-trace --pmc: FETCH_SIZE | WRITE_SIZE | SQ group, "
                   f"separate passes; tools/gpu_pmc_all.sh + tools/pmc_profile.py)",
         "executor": rec["config"]["executor"],
+        "dispatches_per_launch": per_step,
         "fetch_kib_raw": fetch["FETCH_SIZE"],
         "write_kib_raw": write["WRITE_SIZE"],
         "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950; calibrated for 16-byte streaming and 4-byte "
