@@ -446,7 +446,8 @@ def test_c4_full_size_properties(gpu):
 # The other two C4 bench workloads at their bench sizes, through the default
 # heavy kernel (d256: 193 shared slots, the first 160 in LDS and the rest in
 # the wave's HBM block; d1024: 961 shared slots in HBM, wave-blocked buffer
-# slots, 4,096 waves): constant status and steps on
+# slots, four launches of at most 69,824 inputs whose slot blocks fit the
+# Infinity Cache -- tis_jit.h kJitSlotBytes): constant status and steps on
 # every lane (the pipeline's control flow does not depend on x), the
 # counters, and a tail slice bit-exact against the oracle
 # (stack.go:95-155, intStack.go:20-38).
