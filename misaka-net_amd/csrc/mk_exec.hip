@@ -2143,6 +2143,14 @@ bool rtc_spawn(const std::string &helper, HiprtcJob &j, bool &ok, std::string &w
     return ran;
 }
 
+// Code object version of the native tier's modules, in process and in mk_rtc
+// alike: v5, which every HIP runtime a caller may bring understands.  ROCm
+// 7.2's hiprtc defaults to v6; loaded into PyTorch's bundled (ROCm 7.0) HIP
+// runtime, v6 modules of the machine shape left the host heap corrupted at
+// process exit (free(): corrupted unsorted chunks after 60 dynamic-stack
+// networks, r03c-r03k), v5 ones and the bundled compiler's did not.
+constexpr const char *kCodeObjectVersion = "-mcode-object-version=5";
+
 // In-process hiprtc (the linked symbols).
 void rtc_inproc(const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
 {
@@ -2151,8 +2159,8 @@ void rtc_inproc(const std::string &src, bool &ok, std::string &why, std::vector<
         why = "hiprtcCreateProgram failed";
         return;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", kCodeObjectVersion};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
     size_t cs = 0;
     if (r != HIPRTC_SUCCESS) {
         size_t ls = 0;

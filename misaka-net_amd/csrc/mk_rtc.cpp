@@ -37,8 +37,9 @@ int main(int argc, char **argv)
         std::printf("hiprtcCreateProgram failed\n");
         return 1;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    // code object v5, as mk_exec.hip kCodeObjectVersion (why: there)
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
     size_t cs = 0;
     int rc = 0;
     if (r != HIPRTC_SUCCESS) {

@@ -287,3 +287,21 @@ def test_knobs_are_snapshotted_per_network(monkeypatch):
     assert "shape=machine" in net.plan(mode="jit")
     assert "#define MK_JIT_MACHINE 1" in net.jit_source()
     assert "knobs=shape=machine" in net.plan(mode="jit")
+
+
+# The native tier's modules are code object v5 whichever hiprtc builds them
+# (mk_exec.hip kCodeObjectVersion, mk_rtc.cpp): ROCm 7.2's default v6 modules
+# corrupted the host heap inside PyTorch's bundled HIP runtime (r03c-r03k).
+# The module of a dynamic-stack network (the shape that showed it), dumped by
+# MK_JIT_DUMP, read with llvm-readelf: ELF ABI version 3 = code object v5.
+def test_modules_are_code_object_v5(tmp_path, monkeypatch):
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(readelf):
+        pytest.skip("llvm-readelf not installed")
+    rows, _ = stack_loop_network(3)
+    co = str(tmp_path / "m.co")
+    monkeypatch.setenv("MK_JIT_DUMP", co)
+    plan = mk.Network(rows).plan()
+    assert plan.startswith("tier=native"), plan
+    hdr = subprocess.run([readelf, "-h", co], capture_output=True, text=True, check=True).stdout
+    assert any(l.split() == ["ABI", "Version:", "3"] for l in hdr.splitlines()), hdr
