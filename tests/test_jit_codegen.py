@@ -298,7 +298,7 @@ def test_modules_are_code_object_v5(tmp_path, monkeypatch):
     readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
     if not os.path.exists(readelf):
         pytest.skip("llvm-readelf not installed")
-    rows, _ = stack_loop_network(3)
+    rows, _ = stack_loop_network(6)  # two dynamic stacks, machine shape
     co = str(tmp_path / "m.co")
     monkeypatch.setenv("MK_JIT_DUMP", co)
     plan = mk.Network(rows).plan()
