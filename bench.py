@@ -21,15 +21,13 @@ import sys
 import time
 
 import numpy as np
+import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# the package loads its native library (and with it this ROCm's HIP runtime)
-# before PyTorch: misaka_net_amd/__init__.py
 import misaka_net_amd as mk  # noqa: E402
 from misaka_net_amd import _native as N  # noqa: E402
-import torch  # noqa: E402
 
 SEED = 0x4D49534B41
 METRIC = "simulated TIS node-instructions/sec (whole node) + /compute results/sec at 1/2/4/8 GPU"

@@ -11,15 +11,6 @@ if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 
 
-# Build (a no-op when the content stamps match) and load the native library
-# before any test imports PyTorch, as the package does on import
-# (misaka_net_amd/__init__.py): one ROCm compiles and runs the native tier.
-import __graft_entry__ as _g  # noqa: E402
-
-_g.build_native()
-import misaka_net_amd  # noqa: E402,F401
-
-
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: long-running")
