@@ -1538,6 +1538,31 @@ struct DevCtx {
     hipEvent_t ev = nullptr;
 };
 
+// MK_JIT_KEEP_MODULES=1: native modules are never unloaded, and their code
+// objects stay alive with them (a probe of the exit-time heap corruption of
+// helper-compiled modules in PyTorch's bundled runtime).
+inline bool keep_modules()
+{
+    static const bool k = [] {
+        const char *s = std::getenv("MK_JIT_KEEP_MODULES");
+        return s && *s == '1';
+    }();
+    return k;
+}
+
+inline void release_module(hipModule_t mod, std::vector<char> &code)
+{
+    if (!mod) return;
+    if (keep_modules()) {
+        static std::mutex mu;
+        static auto *kept = new std::vector<std::vector<char>>(); // never freed
+        std::lock_guard<std::mutex> g(mu);
+        if (!code.empty()) kept->push_back(std::move(code));
+        return;
+    }
+    (void)hipModuleUnload(mod);
+}
+
 } // namespace mk
 
 struct mk_net {
@@ -1568,7 +1593,7 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_slots);
                 (void)hipFree(sc->dev[d].d_order);
                 (void)hipFree(sc->dev[d].d_ordtab);
-                if (sc->jit.dev[d].mod) (void)hipModuleUnload(sc->jit.dev[d].mod);
+                mk::release_module(sc->jit.dev[d].mod, sc->jit.code);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
             if (c.ev) (void)hipEventDestroy(c.ev);
@@ -2588,7 +2613,7 @@ struct mk_session {
         (void)hipFree(d_native);
         (void)hipFree(d_stage);
         (void)hipHostFree(h_stage);
-        if (mod) (void)hipModuleUnload(mod);
+        mk::release_module(mod, code);
         if (order) (void)hipEventDestroy(order);
         if (stream) (void)hipStreamDestroy(stream);
     }
