@@ -1322,27 +1322,49 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             // (twice the issue cycles per wave): the first iteration, whose x
             // may be any value, uses med3 (MK_JIT_FLAG_MIN=0: med3 throughout).
             const bool fmin = step == -1 && !std::strcmp(flag, "MK_FLAG_GT") && g.lim->flag_min;
-            if (fmin) {
+            if (fmin && g.lim->sat_dec) {
+                // Past the first iteration a lane still in the loop has x > 0:
+                // one saturating decrement per iteration (v_sub_u32 clamp), a
+                // lane that left holds 0 and its flag is x != 0.  Lanes that
+                // left at the first test are parked at 0 and get their x back.
                 e.line("    it = 1u;");
                 e.line("    x = (int32_t)((uint32_t)x - 1u);");
-                e.line("    f = MK_FLAG_GT(x);");
+                e.line("    (void)f;");
+                e.line("    const int32_t f0 = MK_FLAG_GT(x), x0 = x;");
+                e.line("    x = f0 ? x : 0;");
+                if (g.lim->sat_dec == 2) e.line("    const uint32_t one_ = MK_OPAQUE1();");
+                e.line("    more = MK_KEEP(x != 0, need);");
+                e.line("    while (more && T32 - it >= %uu) {", uf);
+                e.line("    it += %uu;", uf);
+                for (int u = 0; u < uf; ++u)
+                    e.line(g.lim->sat_dec == 2 ? "    x = MK_SATSUB(x, one_);" : "    x = MK_SATDEC(x);");
+                e.line("    more = MK_KEEP(x != 0, need);");
+                e.line("    }");
+                e.line("    a = x != 0;");
+                e.line("    x = f0 ? x : x0;");
+            } else {
+                if (fmin) {
+                    e.line("    it = 1u;");
+                    e.line("    x = (int32_t)((uint32_t)x - 1u);");
+                    e.line("    f = MK_FLAG_GT(x);");
+                    e.line("    more = MK_KEEP(f != 0, need);");
+                }
+                e.line("    while (more && T32 - it >= %uu) {", uf);
+                e.line("    it += %uu;", uf);
+                for (int u = 0; u < uf; ++u) {
+                    if (step == 1 || step == -1)
+                        e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)f);", step < 0 ? '-' : '+');
+                    else
+                        e.line("    x = MK_MAD24(f, %d, x);", (int)step);
+                    if (fmin)
+                        e.line("    f = MK_FLAG_MIN(x, f);");
+                    else
+                        e.line("    f = %s(x);", flag);
+                }
                 e.line("    more = MK_KEEP(f != 0, need);");
+                e.line("    }");
+                e.line("    a = f != 0;");
             }
-            e.line("    while (more && T32 - it >= %uu) {", uf);
-            e.line("    it += %uu;", uf);
-            for (int u = 0; u < uf; ++u) {
-                if (step == 1 || step == -1)
-                    e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)f);", step < 0 ? '-' : '+');
-                else
-                    e.line("    x = MK_MAD24(f, %d, x);", (int)step);
-                if (fmin)
-                    e.line("    f = MK_FLAG_MIN(x, f);");
-                else
-                    e.line("    f = %s(x);", flag);
-            }
-            e.line("    more = MK_KEEP(f != 0, need);");
-            e.line("    }");
-            e.line("    a = f != 0;");
         } else {
             phase(LOOP_NARROW, "T32");
         }
@@ -2091,6 +2113,7 @@ JitLimits JitLimits::from_env()
         l.lds_auto = false;
     }
     flag("MK_JIT_FLAG_MIN", l.flag_min);
+    num("MK_JIT_SAT_DEC", l.sat_dec);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
@@ -2106,10 +2129,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,sdec=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)ts_dyn,
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)sat_dec, (int)ts_dyn,
              (int)tune_regs,
              lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad);
     return b;
@@ -2461,6 +2484,13 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool)
     e.line("#define MK_FLAG_NZ(x) mk_flag_nz(x)");
     e.line("#define MK_FLAG_MIN(x, f) mk_flag_min((x), (f))");
     e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
+    // x - 1 saturating at 0 as unsigned (asm: LLVM folds a chain of them into one subtract)
+    e.line("MK_FN int32_t mk_satdec(int32_t x) { int32_t r; __asm__(\"v_sub_u32_e64 %%0, %%1, 1 clamp\" : \"=v\"(r) : \"v\"(x)); return r; }");
+    e.line("#define MK_SATDEC(x) mk_satdec(x)");
+    // the same in plain C, by a 1 that LLVM cannot see (no hazard s_nop after asm)
+    e.line("MK_FN uint32_t mk_opaque1() { uint32_t r; __asm__(\"v_mov_b32 %%0, 1\" : \"=v\"(r)); return r; }");
+    e.line("#define MK_OPAQUE1() mk_opaque1()");
+    e.line("#define MK_SATSUB(x, o) ((int32_t)__builtin_elementwise_sub_sat((uint32_t)(x), (o)))");
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (lim.slot_nt) {
         e.line("#define MK_SLOT_ST(b, ss, s, v) __builtin_nontemporal_store((v), (b) + (uint64_t)(s) * (ss))");

@@ -129,6 +129,11 @@ struct JitLimits {
     // min_u32(x, f), a VOP2 op, after a first iteration by med3 (VOP3)
     // (MK_JIT_FLAG_MIN=0: med3 in every iteration).
     bool flag_min = true;
+    // ... and, past that first iteration, run as one saturating decrement per
+    // iteration (v_sub_u32 x, x, 1 clamp: a lane that left holds 0), the
+    // flag being x != 0 (MK_JIT_SAT_DEC=0: sub + min_u32 per iteration;
+    // 1: inline asm; 2: LLVM's usub.sat by an opaque 1, no hazard s_nop).
+    uint32_t sat_dec = 1;
     // Heavy stream networks whose LDS slots allow fewer than four waves per
     // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
     // mk_exec.hip tune_soft_regs).

@@ -144,6 +144,9 @@ SESS_HEADER = """#include <cstdint>
 #define MK_FLAG_NZ(x) ((int32_t)((x) != 0))
 #define MK_FLAG_MIN(x, f) ((int32_t)((uint32_t)(x) < (uint32_t)(f) ? (uint32_t)(x) : (uint32_t)(f)))
 #define MK_MAD24(f, k, x) ((int32_t)((uint32_t)(x) + (uint32_t)(f) * (uint32_t)(k)))
+#define MK_SATDEC(x) ((int32_t)((uint32_t)(x) ? (uint32_t)(x) - 1u : 0u))
+#define MK_OPAQUE1() 1u
+#define MK_SATSUB(x, o) ((int32_t)((uint32_t)(x) >= (o) ? (uint32_t)(x) - (o) : 0u))
 """
 
 SESS_DRIVER = """
