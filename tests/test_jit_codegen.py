@@ -138,6 +138,20 @@ def test_loop_phases(tmp_path):
     assert len(check_cases(tmp_path, cases, machine=True)) == len(cases)
 
 
+# The countdown's saturating-decrement forms (MK_JIT_SAT_DEC: 0 sub + min_u32,
+# 2 usub.sat by an opaque 1; the default 1 runs in every other test): every
+# loop path, and C5 over all trip counts and at budgets inside its loops.
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_countdown_forms(tmp_path, monkeypatch, mode):
+    monkeypatch.setenv("MK_JIT_SAT_DEC", mode)
+    cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
+    cases.append(("c5_all_trips", mk.networks.countdown_network(), np.arange(-3, 1024, dtype=np.int64), {}))
+    for b in (1, 2, 3, 37, 400, 1500):
+        cases.append((f"c5_budget{b}", mk.networks.countdown_network(),
+                      po.gen_inputs(SEED, 300, kind=1, mask=1023), {"budget": b}))
+    assert len(check_cases(tmp_path, cases, machine=True)) == len(cases)
+
+
 @pytest.mark.parametrize("machine", [False, True])
 @pytest.mark.parametrize("block", range(4))
 def test_random_networks(tmp_path, block, machine):
