@@ -49,6 +49,7 @@ extern char **environ;
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1538,29 +1539,60 @@ struct DevCtx {
     hipEvent_t ev = nullptr;
 };
 
-// MK_JIT_KEEP_MODULES=1: native modules are never unloaded, and their code
-// objects stay alive with them (a probe of the exit-time heap corruption of
-// helper-compiled modules in PyTorch's bundled runtime).
-inline bool keep_modules()
+// Native modules loaded once per (device, code object) and never unloaded:
+// MK_JIT_KEEP_MODULES=1 for every module, =0 for none; unset, the modules a
+// helper process compiled (ROCm 7.2 code objects run by PyTorch's bundled
+// runtime) when kKeepHelperModules.  Networks and sessions
+// whose code objects are equal share one module.
+constexpr bool kKeepHelperModules = false;
+
+inline int keep_policy() // 1 all, 0 none, -1 by compiler
 {
-    static const bool k = [] {
+    static const int k = [] {
         const char *s = std::getenv("MK_JIT_KEEP_MODULES");
-        return s && *s == '1';
+        return s && *s ? (*s == '1' ? 1 : 0) : -1;
     }();
     return k;
 }
 
-inline void release_module(hipModule_t mod, std::vector<char> &code)
+inline bool keep_module(const std::string &from)
 {
-    if (!mod) return;
-    if (keep_modules()) {
-        static std::mutex mu;
-        static auto *kept = new std::vector<std::vector<char>>(); // never freed
-        std::lock_guard<std::mutex> g(mu);
-        if (!code.empty()) kept->push_back(std::move(code));
-        return;
+    const int k = keep_policy();
+    return k == 1 || (k < 0 && kKeepHelperModules && from == "helper");
+}
+
+struct KeptModule {
+    int dev;
+    std::vector<char> code; // the image stays alive with its module
+    hipModule_t mod;
+};
+
+// hipModuleLoadData, or the kept module of an equal code object.  Caller
+// has the device current.
+inline hipError_t load_module(int dev, const std::vector<char> &code, const std::string &from, hipModule_t *mod)
+{
+    if (!keep_module(from)) return hipModuleLoadData(mod, code.data());
+    static std::mutex mu;
+    static auto *kept = new std::deque<KeptModule>(); // never freed
+    std::lock_guard<std::mutex> g(mu);
+    for (const KeptModule &k : *kept)
+        if (k.dev == dev && k.code == code) {
+            *mod = k.mod;
+            return hipSuccess;
+        }
+    kept->push_back(KeptModule{dev, code, nullptr});
+    const hipError_t e = hipModuleLoadData(&kept->back().mod, kept->back().code.data());
+    if (e != hipSuccess) {
+        kept->pop_back();
+        return e;
     }
-    (void)hipModuleUnload(mod);
+    *mod = kept->back().mod;
+    return hipSuccess;
+}
+
+inline void release_module(hipModule_t mod, const std::string &from)
+{
+    if (mod && !keep_module(from)) (void)hipModuleUnload(mod);
 }
 
 } // namespace mk
@@ -1593,7 +1625,7 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_slots);
                 (void)hipFree(sc->dev[d].d_order);
                 (void)hipFree(sc->dev[d].d_ordtab);
-                mk::release_module(sc->jit.dev[d].mod, sc->jit.code);
+                mk::release_module(sc->jit.dev[d].mod, sc->jit.rtc);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
             if (c.ev) (void)hipEventDestroy(c.ev);
@@ -2318,7 +2350,7 @@ int ensure_jit_device(SchedCache *sc, int d)
     JitDev &jd = sc->jit.dev[d];
     if (jd.fn) return MK_OK;
     DeviceGuard g(d);
-    if (hipModuleLoadData(&jd.mod, sc->jit.code.data()) != hipSuccess) return MK_EDEVICE;
+    if (load_module(d, sc->jit.code, sc->jit.rtc, &jd.mod) != hipSuccess) return MK_EDEVICE;
     if (hipModuleGetFunction(&jd.fn, jd.mod, kJitKernel) != hipSuccess) return MK_EDEVICE;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, sc->jit.block, 0) != hipSuccess ||
         jd.per_cu < 1)
@@ -2594,6 +2626,7 @@ struct mk_session {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     std::vector<char> code; // the module's code object: HIP may read the image after hipModuleLoadData
+    std::string rtc_from;   // its compiler (load_module / release_module)
     void *d_native = nullptr; // every native array, one allocation
     size_t native_bytes = 0;
     uint32_t *nsb = nullptr, *hand_sb = nullptr, *hand_steps = nullptr, *hand_call = nullptr;
@@ -2613,7 +2646,7 @@ struct mk_session {
         (void)hipFree(d_native);
         (void)hipFree(d_stage);
         (void)hipHostFree(h_stage);
-        mk::release_module(mod, code);
+        mk::release_module(mod, rtc_from);
         if (order) (void)hipEventDestroy(order);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -2707,7 +2740,8 @@ int session_native(mk_session *s)
     if (!rtc_compile(src, h->jit_lim.max_compile_s, code, why, from)) return decline(why);
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     DeviceGuard g(s->device);
-    if (hipModuleLoadData(&s->mod, code.data()) != hipSuccess ||
+    s->rtc_from = from;
+    if (load_module(s->device, code, from, &s->mod) != hipSuccess ||
         hipModuleGetFunction(&s->fn, s->mod, kJitSessKernel) != hipSuccess)
         return MK_EDEVICE;
     std::vector<SessMapHdr> hdr;
