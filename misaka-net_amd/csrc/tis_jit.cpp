@@ -2426,7 +2426,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 namespace {
 // Everything a module needs before its lane code: types, status codes,
 // policy, the flag / loop helpers, the slot-access macros, mk_device_common.
-std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool)
+std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, bool sat)
 {
     Emitter e;
     if (shape == JIT_MACHINE && pool >= 64) e.line("#define MK_POOL %uu", pool);
@@ -2484,13 +2484,17 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool)
     e.line("#define MK_FLAG_NZ(x) mk_flag_nz(x)");
     e.line("#define MK_FLAG_MIN(x, f) mk_flag_min((x), (f))");
     e.line("#define MK_MAD24(f, k, x) mk_mad24((f), (k), (x))");
-    // x - 1 saturating at 0 as unsigned (asm: LLVM folds a chain of them into one subtract)
-    e.line("MK_FN int32_t mk_satdec(int32_t x) { int32_t r; __asm__(\"v_sub_u32_e64 %%0, %%1, 1 clamp\" : \"=v\"(r) : \"v\"(x)); return r; }");
-    e.line("#define MK_SATDEC(x) mk_satdec(x)");
-    // the same in plain C, by a 1 that LLVM cannot see (no hazard s_nop after asm)
-    e.line("MK_FN uint32_t mk_opaque1() { uint32_t r; __asm__(\"v_mov_b32 %%0, 1\" : \"=v\"(r)); return r; }");
-    e.line("#define MK_OPAQUE1() mk_opaque1()");
-    e.line("#define MK_SATSUB(x, o) ((int32_t)__builtin_elementwise_sub_sat((uint32_t)(x), (o)))");
+    // the saturating countdown forms (emit_self_loop), only in modules that
+    // use them (other modules' source -- and its hash -- stays as it was)
+    if (sat) {
+        // x - 1 saturating at 0 as unsigned (asm: LLVM folds a chain of them into one subtract)
+        e.line("MK_FN int32_t mk_satdec(int32_t x) { int32_t r; __asm__(\"v_sub_u32_e64 %%0, %%1, 1 clamp\" : \"=v\"(r) : \"v\"(x)); return r; }");
+        e.line("#define MK_SATDEC(x) mk_satdec(x)");
+        // the same in plain C, by a 1 that LLVM cannot see (no hazard s_nop after asm)
+        e.line("MK_FN uint32_t mk_opaque1() { uint32_t r; __asm__(\"v_mov_b32 %%0, 1\" : \"=v\"(r)); return r; }");
+        e.line("#define MK_OPAQUE1() mk_opaque1()");
+        e.line("#define MK_SATSUB(x, o) ((int32_t)__builtin_elementwise_sub_sat((uint32_t)(x), (o)))");
+    }
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (lim.slot_nt) {
         e.line("#define MK_SLOT_ST(b, ss, s, v) __builtin_nontemporal_store((v), (b) + (uint64_t)(s) * (ss))");
@@ -2610,7 +2614,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
                               uint32_t pool)
 {
     Emitter e;
-    e.s = module_prelude(shape, lim, pool);
+    e.s = module_prelude(shape, lim, pool, lane_src.find("MK_SAT") != std::string::npos);
     e.s += lane_src;
     const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
@@ -2633,7 +2637,7 @@ bool jit_session_source(const SchedProgram &p, const JitLimits &lim, std::string
     if (!analyze(p, lim, g, why)) return false;
     Emitter e;
     emit_machine_lane(p, g, e);
-    src = module_prelude(JIT_MACHINE, lim, 0) + e.s + kSessionKernel;
+    src = module_prelude(JIT_MACHINE, lim, 0, e.s.find("MK_SAT") != std::string::npos) + e.s + kSessionKernel;
     return true;
 }
 
