@@ -15,7 +15,9 @@
  *   {"client": "c", "workload": ..., "lanes": N, "steps": K, "ms_per_step": T,
  *    "node_instr_per_s": V, "plan": "..."}
  *
- *   mk_bench [c2 | c4:D] [steps] [warmup]
+ * "c5" = the countdown network (networks.py countdown_network), 4,194,304
+ * lanes of inputs masked to 0..1023 (bench.py's MK_GEN_MASKED generator).
+ *   mk_bench [c2 | c4:D | c5] [steps] [warmup]
  * Exit codes: 0 ok, 2 load failed, 3 device / compute failed.
  */
 #include <hip/hip_runtime_api.h>
@@ -28,6 +30,10 @@
 
 static const char *MISAKA1 = "IN ACC\nADD 1\nMOV ACC, misaka2:R0\nMOV R0, ACC\nOUT ACC\n";
 static const char *MISAKA2 = "MOV R0, ACC\nADD 1\nPUSH ACC, misaka3\nPOP misaka3, ACC\nMOV ACC, misaka1:R0\n";
+/* networks.py countdown_network (C5) */
+static const char *COUNT = "IN ACC\nSAV\nL: SUB 1\nJGZ L\nSWP\nMOV ACC, digits:R0\n";
+static const char *DIGITS = "MOV R0, ACC\nJEZ Z\nJLZ Z\nL: SUB 3\nJGZ L\nADD 3\nJRO ACC\nADD 100\nADD 10\nADD 1\n"
+                            "OUT ACC\nJMP E\nZ: OUT -1\nE: NOP\n";
 
 /* networks.py pipeline_program(k, nodes, depth), line for line */
 static char *pipeline_program(int k, int nodes, int depth)
@@ -64,12 +70,19 @@ int main(int argc, char **argv)
     char *progs[8] = {0};
     int nn = 0;
     size_t lanes = 0;
+    uint32_t gen_kind = MK_GEN_FULL, gen_mask = 0; /* bench.py WORKLOADS' generator */
     if (!strcmp(wl, "c2")) {
         nodes[0] = (mk_node_desc){"misaka1", MK_NODE_PROGRAM, MISAKA1};
         nodes[1] = (mk_node_desc){"misaka2", MK_NODE_PROGRAM, MISAKA2};
         nodes[2] = (mk_node_desc){"misaka3", MK_NODE_STACK, NULL};
         nn = 3;
         lanes = (size_t)1 << 24;
+    } else if (!strcmp(wl, "c5")) {
+        nodes[0] = (mk_node_desc){"count", MK_NODE_PROGRAM, COUNT};
+        nodes[1] = (mk_node_desc){"digits", MK_NODE_PROGRAM, DIGITS};
+        nn = 2;
+        lanes = (size_t)1 << 22;
+        gen_kind = MK_GEN_MASKED, gen_mask = 1023;
     } else if (!strncmp(wl, "c4:", 3)) {
         const int depth = atoi(wl + 3);
         for (int k = 0; k < 8; ++k) {
@@ -108,7 +121,7 @@ int main(int argc, char **argv)
     CHECK_HIP(hipMalloc((void **)&d_st, lanes));
     CHECK_HIP(hipMalloc((void **)&d_stats, 8 * sizeof(uint64_t)));
     CHECK_HIP(hipMemset(d_stats, 0, 8 * sizeof(uint64_t)));
-    if (mk_generate_inputs_device(0, 0x4D49534B41ull, MK_GEN_FULL, 0, 0, lanes, d_in, s) != MK_OK) return 3;
+    if (mk_generate_inputs_device(0, 0x4D49534B41ull, gen_kind, gen_mask, 0, lanes, d_in, s) != MK_OK) return 3;
     mk_input in;
     memset(&in, 0, sizeof in);
     in.kind = MK_IN_I32;

@@ -107,25 +107,26 @@ def _build_c_bench(tmp_path):
     return exe
 
 
-@pytest.mark.parametrize("depth", [64, 256, 1024])
+@pytest.mark.parametrize("depth", [64, 256, 1024, "c5"])
 def test_c_bench_networks_match_bench_py(tmp_path, depth):
     # the C timing client runs bench.py's networks: same program text
     import subprocess
 
     exe = _build_c_bench(tmp_path)
-    r = subprocess.run([exe, f"c4:{depth}", "print"], capture_output=True, text=True, check=True)
+    wl = depth if depth == "c5" else f"c4:{depth}"
+    r = subprocess.run([exe, wl, "print"], capture_output=True, text=True, check=True)
     got = {}
     for block in r.stdout.split("== ")[1:]:
         head, _, text = block.partition("\n")
         name, kind = head.split()
         got[name] = (int(kind), text)
     want = {n.name: ({"program": 0, "stack": 1}[n.kind], n.program if n.kind == "program" else "")
-            for n in mk.networks.pipeline_network(depth)}
+            for n in (mk.networks.countdown_network() if depth == "c5" else mk.networks.pipeline_network(depth))}
     assert got == want
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wl", ["c2", "c4:64"])
+@pytest.mark.parametrize("wl", ["c2", "c4:64", "c5"])
 def test_c_bench_on_gpu(gpu, tmp_path, wl):
     import json
     import subprocess
