@@ -27,7 +27,11 @@
 #include <hip/hiprtc.h>
 
 #include <dlfcn.h>
+#include <execinfo.h>
 #include <fcntl.h>
+#include <pthread.h>
+#include <ucontext.h>
+#include <sys/syscall.h>
 #include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>
@@ -50,6 +54,7 @@ extern char **environ;
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1495,7 +1500,7 @@ struct JitState {
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
     bool lds = false;                // heavy kernel with all its stack slots in LDS (no HBM slots)
     uint32_t lds_n = 0;              // heavy kernel: slots per lane in LDS (the rest in HBM)
-    std::string rtc;                 // compiler of the module: "helper" (mk_rtc) or "inproc"
+    std::string rtc;                 // compiler of the module: linked / ns / helper / linked-other
     uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
@@ -2086,15 +2091,133 @@ struct HiprtcJob {
 
 // Compiles still running on detached threads: the library's teardown waits
 // for them (a thread inside comgr while static destructors run would crash).
+// Diagnostics (MK_SEGV_TRACE=1): a fatal signal in any thread prints that
+// thread's native backtrace (library+offset per frame) before the handler
+// that was installed before it (Python's faulthandler, say) runs.
+struct sigaction g_prev_segv, g_prev_bus, g_prev_abrt;
+void segv_trace(int sig, siginfo_t *si, void *uc)
+{
+    // async-signal-safe after the warm-up at install: no malloc here
+    char msg[256];
+    const auto *ctx = static_cast<const ucontext_t *>(uc);
+    void *pc = ctx ? reinterpret_cast<void *>(ctx->uc_mcontext.gregs[REG_RIP]) : nullptr;
+    Dl_info info{};
+    const bool named = pc && dladdr(pc, &info) && info.dli_fname;
+    char comm[32] = "?";
+    {
+        char path[64];
+        snprintf(path, sizeof path, "/proc/self/task/%ld/comm", (long)syscall(SYS_gettid));
+        const int fd = open(path, O_RDONLY);
+        if (fd >= 0) {
+            const ssize_t r = read(fd, comm, sizeof comm - 1);
+            comm[r > 0 ? r - 1 : 0] = 0;
+            close(fd);
+        }
+    }
+    const int l = snprintf(msg, sizeof msg, "mk: signal %d at %p in thread %ld (%s), pc %p = %s+%#lx\n", sig,
+                           si ? si->si_addr : nullptr, (long)syscall(SYS_gettid), comm, pc,
+                           named ? info.dli_fname : "?",
+                           named ? (unsigned long)((char *)pc - (char *)info.dli_fbase) : 0ul);
+    if (write(2, msg, (size_t)l) < 0) {
+    }
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    backtrace_symbols_fd(frames, n, 2);
+    const struct sigaction &prev = sig == SIGSEGV ? g_prev_segv : sig == SIGBUS ? g_prev_bus : g_prev_abrt;
+    if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
+        prev.sa_sigaction(sig, si, uc);
+        return;
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct SegvTrace {
+    SegvTrace()
+    {
+        const char *e = std::getenv("MK_SEGV_TRACE");
+        if (!e || *e != '1') return;
+        void *warm[2];
+        (void)backtrace(warm, 2); // loads the unwinder now, not inside the handler
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = segv_trace;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigaction(SIGSEGV, &sa, &g_prev_segv);
+        sigaction(SIGBUS, &sa, &g_prev_bus);
+        sigaction(SIGABRT, &sa, &g_prev_abrt);
+        on = true;
+    }
+    bool on = false;
+} g_segv_trace;
+
+// Diagnostics: a compiler that installed its own fatal-signal handlers is
+// named, and ours put back in front of them.
+void segv_trace_check()
+{
+    if (!g_segv_trace.on) return;
+    struct sigaction cur;
+    if (sigaction(SIGSEGV, nullptr, &cur) || cur.sa_sigaction == segv_trace) return;
+    Dl_info info{};
+    const bool named = dladdr(reinterpret_cast<void *>(cur.sa_sigaction), &info) && info.dli_fname;
+    fprintf(stderr, "mk: SIGSEGV handler replaced by %s; reinstalled\n", named ? info.dli_fname : "?");
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
+}
+
+// Compile threads: detached, with a stack of their own size.  Clang and LLVM
+// recurse deeply on long generated sources; a thread's default stack is the
+// stack rlimit (8 MiB here) or 2 MiB where that rlimit is unlimited, less
+// than the main thread of a compiler process gets.  With MK_SEGV_TRACE the
+// thread also gets an alternate signal stack, so an overflow is reported.
+constexpr size_t kCompileStack = (size_t)256 << 20;
+
+void *compile_thread_main(void *arg)
+{
+    std::unique_ptr<std::function<void()>> f(static_cast<std::function<void()> *>(arg));
+    if (g_segv_trace.on) {
+        stack_t ss{};
+        ss.ss_size = 1 << 16;
+        ss.ss_sp = std::malloc(ss.ss_size); // held for the thread's life
+        if (ss.ss_sp) (void)sigaltstack(&ss, nullptr);
+    }
+    (*f)();
+    return nullptr;
+}
+
+bool spawn_compile_thread(std::function<void()> fn)
+{
+    auto *f = new std::function<void()>(std::move(fn));
+    pthread_attr_t a;
+    pthread_attr_init(&a);
+    pthread_attr_setstacksize(&a, kCompileStack);
+    pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
+    pthread_t t;
+    const int rc = pthread_create(&t, &a, compile_thread_main, f);
+    pthread_attr_destroy(&a);
+    if (rc) {
+        // no thread: run here (the caller's stack)
+        std::unique_ptr<std::function<void()>> own(f);
+        (*own)();
+        return false;
+    }
+    return true;
+}
+
 std::mutex g_rtc_mu;
 std::condition_variable g_rtc_cv;
 int g_rtc_running = 0;
+void rtc_drain_at_exit()
+{
+    std::unique_lock<std::mutex> lk(g_rtc_mu);
+    (void)g_rtc_cv.wait_for(lk, std::chrono::seconds(120), [] { return g_rtc_running == 0; });
+}
 struct RtcDrain {
-    ~RtcDrain()
-    {
-        std::unique_lock<std::mutex> lk(g_rtc_mu);
-        (void)g_rtc_cv.wait_for(lk, std::chrono::seconds(120), [] { return g_rtc_running == 0; });
-    }
+    ~RtcDrain() { rtc_drain_at_exit(); }
 } g_rtc_drain;
 
 // The native tier's compiler is this ROCm install's hiprtc, always: a cgo or
@@ -2102,23 +2225,28 @@ struct RtcDrain {
 // imported PyTorch first, PyTorch's bundled libhiprtc / libamd_comgr (the
 // same sonames, an older LLVM) are what the linked hiprtc symbols resolve to
 // -- a different compiler, whose code differs from network to network (C4
-// D=256: 132 VGPRs against 75).  There the module is compiled by mk_rtc
-// (csrc/mk_rtc.cpp, built next to this library), a child process that loads
-// this ROCm's compiler, so every caller gets the same module.  The
-// in-process hiprtc is the fallback when the helper is missing or fails, or
-// with MK_HIPRTC=linked; MK_HIPRTC=<path> names another helper.
-std::string rtc_helper()
-{
-    const char *e = std::getenv("MK_HIPRTC");
-    if (e && *e) return std::strcmp(e, "linked") ? std::string(e) : std::string();
-    Dl_info info{};
-    if (!dladdr(reinterpret_cast<void *>(&rtc_helper), &info) || !info.dli_fname) return {};
-    std::string dir(info.dli_fname);
-    const size_t slash = dir.rfind('/');
-    dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
-    const std::string path = dir + "/mk_rtc";
-    return access(path.c_str(), X_OK) == 0 ? path : std::string();
-}
+// D=256: 132 VGPRs against 75).  There this ROCm's libhiprtc is opened a
+// second time in a link-map namespace of its own (dlmopen LM_ID_NEWLM: its
+// libamd_comgr, libstdc++ and libc come with it, invisible to the rest of
+// the process), and the module is compiled in process by that copy, so
+// every caller gets the same module without a child process.
+//
+// Round 3 compiled such modules in a child process (mk_rtc, posix_spawn from
+// a compile thread); the host heap of those PyTorch processes was found
+// corrupted at exit.  The helper stays available by name only
+// (MK_HIPRTC=helper, or MK_HIPRTC=<path of a helper>); MK_HIPRTC=linked
+// compiles with whatever hiprtc the process resolved (PyTorch's in a PyTorch
+// process).
+#ifndef MK_ROCM_LIB
+#define MK_ROCM_LIB "/opt/rocm/lib"
+#endif
+
+enum RtcKind { RTC_LINKED, RTC_NS, RTC_HELPER };
+
+struct RtcChoice {
+    RtcKind kind = RTC_LINKED;
+    std::string helper; // RTC_HELPER: the executable
+};
 
 // Whether the linked hiprtc is another install's than this ROCm's (PyTorch's
 // bundled one in a process that imported it first).
@@ -2126,8 +2254,150 @@ bool inproc_rtc_differs()
 {
     Dl_info info{};
     if (!dladdr(reinterpret_cast<void *>(&hiprtcCompileProgram), &info) || !info.dli_fname) return false;
-    return std::strncmp(info.dli_fname, "/opt/rocm", 9) != 0;
+    char real[PATH_MAX], want[PATH_MAX];
+    if (!realpath(info.dli_fname, real) || !realpath(MK_ROCM_LIB, want)) return true;
+    const size_t n = std::strlen(want);
+    return std::strncmp(real, want, n) != 0 || real[n] != '/';
 }
+
+RtcChoice rtc_choice()
+{
+    RtcChoice c;
+    const char *e = std::getenv("MK_HIPRTC");
+    if (e && *e) {
+        if (!std::strcmp(e, "linked")) return c;
+        if (!std::strcmp(e, "ns")) {
+            c.kind = RTC_NS;
+            return c;
+        }
+        c.kind = RTC_HELPER;
+        if (std::strcmp(e, "helper")) {
+            c.helper = e;
+            return c;
+        }
+        Dl_info info{};
+        if (dladdr(reinterpret_cast<void *>(&rtc_choice), &info) && info.dli_fname) {
+            std::string dir(info.dli_fname);
+            const size_t slash = dir.rfind('/');
+            dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
+            if (access((dir + "/mk_rtc").c_str(), X_OK) == 0) c.helper = dir + "/mk_rtc";
+        }
+        return c;
+    }
+    if (inproc_rtc_differs()) c.kind = RTC_NS;
+    return c;
+}
+
+// The hiprtc entry points one compile uses: the linked ones, or this ROCm's
+// in its own namespace.
+struct RtcApi {
+    decltype(&hiprtcCreateProgram) create;
+    decltype(&hiprtcCompileProgram) compile;
+    decltype(&hiprtcGetProgramLogSize) log_size;
+    decltype(&hiprtcGetProgramLog) log;
+    decltype(&hiprtcGetCodeSize) code_size;
+    decltype(&hiprtcGetCode) code;
+    decltype(&hiprtcDestroyProgram) destroy;
+    decltype(&hiprtcGetErrorString) error;
+    char ***environ_ns = nullptr; // the namespace libc's environ (null: the linked one)
+};
+
+const RtcApi kLinkedRtc = {&hiprtcCreateProgram, &hiprtcCompileProgram, &hiprtcGetProgramLogSize,
+                           &hiprtcGetProgramLog, &hiprtcGetCodeSize,    &hiprtcGetCode,
+                           &hiprtcDestroyProgram, &hiprtcGetErrorString};
+
+void rtc_drain_at_exit();
+
+// This ROCm's hiprtc in a namespace of its own, opened once per process and
+// never closed; null (with the reason) when it cannot be opened.
+const RtcApi *ns_rtc(std::string &why)
+{
+    static std::string fail;
+    static const RtcApi *api = []() -> const RtcApi * {
+        void *h = dlmopen(LM_ID_NEWLM, MK_ROCM_LIB "/libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char *d = dlerror();
+            fail = std::string("dlmopen: ") + (d ? d : "failed");
+            return nullptr;
+        }
+        auto *a = new RtcApi{};
+        a->create = reinterpret_cast<decltype(a->create)>(dlsym(h, "hiprtcCreateProgram"));
+        a->compile = reinterpret_cast<decltype(a->compile)>(dlsym(h, "hiprtcCompileProgram"));
+        a->log_size = reinterpret_cast<decltype(a->log_size)>(dlsym(h, "hiprtcGetProgramLogSize"));
+        a->log = reinterpret_cast<decltype(a->log)>(dlsym(h, "hiprtcGetProgramLog"));
+        a->code_size = reinterpret_cast<decltype(a->code_size)>(dlsym(h, "hiprtcGetCodeSize"));
+        a->code = reinterpret_cast<decltype(a->code)>(dlsym(h, "hiprtcGetCode"));
+        a->destroy = reinterpret_cast<decltype(a->destroy)>(dlsym(h, "hiprtcDestroyProgram"));
+        a->error = reinterpret_cast<decltype(a->error)>(dlsym(h, "hiprtcGetErrorString"));
+        a->environ_ns = reinterpret_cast<char ***>(dlsym(h, "__environ"));
+        if (!a->create || !a->compile || !a->log_size || !a->log || !a->code_size || !a->code || !a->destroy ||
+            !a->error || !a->environ_ns) {
+            fail = "dlmopen: hiprtc symbols missing";
+            delete a;
+            return nullptr;
+        }
+        // The namespace's static destructors were registered with exit()
+        // while it loaded; a compile still running must end before they run,
+        // so this drain (registered after them) runs first.
+        (void)std::atexit(rtc_drain_at_exit);
+        return a;
+    }();
+    why = fail;
+    return api;
+}
+
+// Every compile in the namespace runs on this one thread, which also opens
+// it, and which never exits.  The namespace's libc keeps per-thread state
+// (ctype tables, malloc's thread cache, thread_local destructor lists) that
+// only the opening thread gets initialised, and that threads started by the
+// process's own libc leave behind unrun when they end: compiles on
+// short-lived threads crashed now and then in comgr (r04a, CPU reproduction).
+class NsCompiler {
+  public:
+    static NsCompiler &get()
+    {
+        static NsCompiler *w = new NsCompiler(); // never destroyed: the thread outlives every caller
+        return *w;
+    }
+    // Runs f on the compile thread and returns when it has.
+    void run(const std::function<void()> &f)
+    {
+        auto done = std::make_shared<std::pair<std::mutex, std::condition_variable>>();
+        bool finished = false;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back([&f, &finished, done] {
+                f();
+                std::lock_guard<std::mutex> g(done->first);
+                finished = true;
+                done->second.notify_all();
+            });
+        }
+        cv_.notify_one();
+        std::unique_lock<std::mutex> lk(done->first);
+        done->second.wait(lk, [&] { return finished; });
+    }
+
+  private:
+    NsCompiler() { spawn_compile_thread([this] { loop(); }); }
+    void loop()
+    {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !q_.empty(); });
+                job = std::move(q_.front());
+                q_.pop_front();
+            }
+            job();
+            segv_trace_check();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+};
 
 bool write_file(const std::string &path, const std::string &data)
 {
@@ -2208,43 +2478,87 @@ bool rtc_spawn(const std::string &helper, HiprtcJob &j, bool &ok, std::string &w
 // networks, r03c-r03k), v5 ones and the bundled compiler's did not.
 constexpr const char *kCodeObjectVersion = "-mcode-object-version=5";
 
-// In-process hiprtc (the linked symbols).
-void rtc_inproc(const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+// The namespace's libc took the process's environment pointer when it was
+// opened, and setenv (os.environ[...] = ... in Python) later reallocates and
+// frees that array: comgr's getenv then read freed memory (r04: SIGSEGV in
+// the compile thread after a test's monkeypatch.setenv).  Each compile gives
+// the namespace a private copy of the current environment instead; only the
+// compile thread touches it.
+void ns_environ_refresh(const RtcApi &rt)
 {
+    static std::vector<std::string> strings;
+    static std::vector<char *> ptrs;
+    std::vector<std::string> s;
+    for (char **e = environ; e && *e; ++e) s.emplace_back(*e);
+    std::vector<char *> p;
+    p.reserve(s.size() + 1);
+    for (std::string &x : s) p.push_back(&x[0]);
+    p.push_back(nullptr);
+    *rt.environ_ns = p.data(); // the new copy is complete before the old one goes
+    strings.swap(s);
+    ptrs.swap(p);
+}
+
+// In-process hiprtc (the linked symbols, or this ROCm's namespace copy).
+void rtc_inproc(const RtcApi &rt, const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+{
+    if (rt.environ_ns) ns_environ_refresh(rt);
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (rt.create(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         why = "hiprtcCreateProgram failed";
         return;
     }
     const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", kCodeObjectVersion};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    const hiprtcResult r = rt.compile(prog, 4, opts);
     size_t cs = 0;
     if (r != HIPRTC_SUCCESS) {
         size_t ls = 0;
-        (void)hiprtcGetProgramLogSize(prog, &ls);
+        (void)rt.log_size(prog, &ls);
         std::string log(ls, '\0');
-        if (ls) (void)hiprtcGetProgramLog(prog, &log[0]);
-        why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
-    } else if (hiprtcGetCodeSize(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
+        if (ls) (void)rt.log(prog, &log[0]);
+        why = std::string("hiprtc: ") + rt.error(r) + ": " + log.substr(0, 400);
+    } else if (rt.code_size(prog, &cs) != HIPRTC_SUCCESS || cs == 0) {
         why = "hiprtc produced no code";
     } else {
         code.resize(cs);
-        (void)hiprtcGetCode(prog, code.data());
+        (void)rt.code(prog, code.data());
         ok = true;
     }
-    (void)hiprtcDestroyProgram(&prog);
+    (void)rt.destroy(&prog);
 }
 
+bool rtc_abandoned(HiprtcJob &j)
+{
+    std::lock_guard<std::mutex> lk(j.mu);
+    return j.abandoned;
+}
+
+// One compile with the chosen compiler.  The linked hiprtc is the fallback
+// when the chosen one cannot run -- unless the caller has given up by then,
+// whose result nobody would read.
 void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
 {
     bool ok = false;
     std::string why;
     std::vector<char> code;
-    const std::string helper = inproc_rtc_differs() ? rtc_helper() : std::string();
-    const bool spawned = !helper.empty() && rtc_spawn(helper, *j, ok, why, code);
-    std::string from = "helper";
-    if (!spawned) {
-        rtc_inproc(j->src, ok, why, code);
+    const RtcChoice ch = rtc_choice();
+    bool ran = false;
+    std::string from;
+    if (ch.kind == RTC_HELPER && !ch.helper.empty()) {
+        ran = rtc_spawn(ch.helper, *j, ok, why, code);
+        from = "helper";
+    } else if (ch.kind == RTC_NS) {
+        NsCompiler::get().run([&] {
+            if (const RtcApi *rt = ns_rtc(why)) {
+                rtc_inproc(*rt, j->src, ok, why, code);
+                ran = true;
+                from = "ns";
+            }
+        });
+    }
+    if (!ran && !rtc_abandoned(*j)) {
+        why.clear();
+        rtc_inproc(kLinkedRtc, j->src, ok, why, code);
         from = inproc_rtc_differs() ? "linked-other" : "linked";
     }
     if (ok) why = from; // which compiler's module (mk_net_plan)
@@ -2274,11 +2588,16 @@ bool rtc_compile(const std::string &src, double max_s, std::vector<char> &code, 
 {
     auto job = std::make_shared<HiprtcJob>();
     job->src = src;
+    if (const char *d = std::getenv("MK_JIT_DUMP_SRC"); d && *d) { // diagnostics: every source, before it compiles
+        char name[64];
+        snprintf(name, sizeof name, "/%016llx.hip", (unsigned long long)src_hash(src));
+        (void)write_file(std::string(d) + name, src);
+    }
     {
         std::lock_guard<std::mutex> lk(g_rtc_mu);
         ++g_rtc_running;
     }
-    std::thread(hiprtc_run, job).detach();
+    spawn_compile_thread([job] { hiprtc_run(job); });
     std::unique_lock<std::mutex> lk(job->mu);
     const auto limit = std::chrono::duration<double>(max_s);
     if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
