@@ -468,31 +468,25 @@ def main():
     # `value`, which stays the sharded compute (no data-path collective).
     e2e = None
     if dist and (world > 1 or args.gather):
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        for _ in range(args.steps):
-            step(False)
-            g_out = mk.dist.gather_outputs(out, dist)
-            g_st = mk.dist.gather_outputs(st, dist)
-        torch.cuda.synchronize()
-        tt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        e2e_s = tt.item()
+        e2e_s, g_out, g_st = mk.dist.timed_gather(lambda: step(False), out, st, dist, args.steps,
+                                                  sync=torch.cuda.synchronize)
         e2e = {"value": None, "ms_per_step": e2e_s / args.steps * 1e3,
                "gathered_bytes_per_step": 5 * lanes * world, "collective": "ordered gather to rank 0 "
                f"({dist.get_backend()}), outputs int32 + status u8"}
         if args.verify_gather and rank == 0:
             # the gathered shards == one launch over all world x lanes global lanes
-            xf = torch.empty(lanes * world, dtype=torch.int32, device="cuda")
-            mk.generate_inputs_device(lanes * world, xf.data_ptr(), seed=SEED, gen_kind=gen_kind, gen_mask=mask,
-                                      offset=0, device=dev, stream=sh)
-            of = torch.empty_like(xf)
-            sf = torch.empty(lanes * world, dtype=torch.uint8, device="cuda")
-            net.compute_device(lanes * world, out_ptr=of.data_ptr(), status_ptr=sf.data_ptr(), in_ptr=xf.data_ptr(),
-                               device=dev, stream=sh, mode=args.mode)
-            torch.cuda.synchronize()
-            e2e["verified"] = bool(torch.equal(of, g_out) and torch.equal(sf, g_st))
+            def full():
+                xf = torch.empty(lanes * world, dtype=torch.int32, device="cuda")
+                mk.generate_inputs_device(lanes * world, xf.data_ptr(), seed=SEED, gen_kind=gen_kind,
+                                          gen_mask=mask, offset=0, device=dev, stream=sh)
+                of = torch.empty_like(xf)
+                sf = torch.empty(lanes * world, dtype=torch.uint8, device="cuda")
+                net.compute_device(lanes * world, out_ptr=of.data_ptr(), status_ptr=sf.data_ptr(),
+                                   in_ptr=xf.data_ptr(), device=dev, stream=sh, mode=args.mode)
+                torch.cuda.synchronize()
+                return of, sf
+
+            e2e["verified"] = mk.dist.verify_gathered(g_out, g_st, full)
             assert e2e["verified"], "gathered outputs differ from a single launch over the global lanes"
 
     host_io = None

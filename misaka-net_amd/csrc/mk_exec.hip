@@ -2951,6 +2951,10 @@ struct mk_session {
     uint32_t *nsb = nullptr, *hand_sb = nullptr, *hand_steps = nullptr, *hand_call = nullptr;
     uint32_t *sflags = nullptr; // SessParams::sflags
     uint32_t epoch = 0;         // native launches so far (never 0 after the first)
+    // A launch whose native kernel ran but whose import / interpreter launch
+    // failed leaves handed-off sessions that no kernel will serve again:
+    // every call then fails (MK_EDEVICE) until mk_session_reset.
+    bool broken = false;
     hipEvent_t order = nullptr; // orders caller streams against the session's stream
     int64_t *regs = nullptr;
     int32_t *slots = nullptr;
@@ -2993,6 +2997,7 @@ struct SessK {
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
                    hipStream_t stream, uint32_t ncalls = 1, bool resume = false)
 {
+    if (s->broken) return MK_EDEVICE;
     if (s->n == 0 || ncalls == 0) return MK_OK;
     SessParams p = s->p;
     p.ncalls = ncalls;
@@ -3019,14 +3024,18 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
                      s->slots, s->hdr, s->rec, s->dyn_base};
         void *iargs[] = {(void *)&q, (void *)&p};
         if (hipLaunchKernel(reinterpret_cast<void *>(&tis_session_import), dim3((unsigned)blocks), dim3(kBlock), iargs,
-                            0, stream) != hipSuccess)
+                            0, stream) != hipSuccess) {
+            s->broken = true;
             return MK_EDEVICE;
+        }
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
     if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)blocks), dim3(kBlock), args, lds, stream) !=
-        hipSuccess)
+        hipSuccess) {
+        if (s->native && !resume) s->broken = true;
         return MK_EDEVICE;
+    }
     return MK_OK;
 }
 
@@ -3360,7 +3369,9 @@ int mk_session_reset(mk_session *s)
     mk::DeviceGuard g(s->device);
     if (hipMemsetAsync(s->d_state, 0, s->state_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
     if (s->native && hipMemsetAsync(s->d_native, 0, s->native_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
-    return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
+    s->broken = false; // every session back to its initial state, none handed off
+    return MK_OK;
 }
 
 int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t ncalls, int32_t *d_out,

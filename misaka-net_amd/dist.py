@@ -41,3 +41,38 @@ def gather_outputs(out, dist, dst: int = 0):
         return buf
     dist.gather(out, dst=dst)
     return None
+
+
+def timed_gather(step, out, status, dist, steps: int, sync=None):
+    """End-to-end leg of an N-rank run (SURVEY.md section 8 row e): `steps`
+    times, run one step (`step()`, the launch that fills this rank's `out`
+    int32 and `status` u8 shards) and gather both to rank 0 in global lane
+    order.  Returns (seconds, the max over ranks; gathered out; gathered
+    status), the gathered tensors on rank 0 and None elsewhere.  `sync`
+    waits for the device (torch.cuda.synchronize); None on CPU."""
+    import time
+
+    import torch
+
+    sync = sync or (lambda: None)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    g_out = g_st = None
+    for _ in range(steps):
+        step()
+        g_out = gather_outputs(out, dist)
+        g_st = gather_outputs(status, dist)
+    sync()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=out.device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return tt.item(), g_out, g_st
+
+
+def verify_gathered(g_out, g_st, full) -> bool:
+    """Rank 0: the gathered shards equal one evaluation over all global lanes
+    (`full()` returns that evaluation's (out, status))."""
+    import torch
+
+    of, sf = full()
+    return bool(torch.equal(of.to(g_out.device), g_out) and torch.equal(sf.to(g_st.device), g_st))

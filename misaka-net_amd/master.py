@@ -177,7 +177,17 @@ class MasterNode:
         self.programs = {k: "" for k, v in self.node_info.items() if v.get("type") == "program"}
         self.devices, self.budget, self.stack_cap = devices, budget, stack_cap
         self.is_running = False
+        # Locks, always taken in this order: _lock guards the control state
+        # (programs, the network and session handles, _epoch) and serialises
+        # /run /pause /reset /load; _burst serialises stateful bursts (one
+        # open call at a time); _exec is held for one executor launch.  A
+        # stateful burst holds _exec per launch only, so /reset, /pause and
+        # /load wait at most one budget slice, never a whole call:
+        # they bump _epoch, and a burst that sees it changed stops resuming.
         self._lock = threading.Lock()
+        self._burst = threading.Lock()
+        self._exec = threading.Lock()
+        self._epoch = 0
         # cmd/app.go:21-24: a PROGRAM that fails to load is logged and the node
         # keeps its default program ([["NOP"]], program.go:64)
         for k, text in (programs or {}).items():
@@ -220,60 +230,80 @@ class MasterNode:
             self._sess = self.network().sessions(1, device=dev, budget=self.budget, stack_cap=self.stack_cap)
         return self._sess
 
-    def _drop_state(self):
+    def _drop_state(self, keep_session: bool = False):
+        """Caller holds _lock and _exec.  /reset keeps the compiled session
+        and clears its state (mk_session_reset); /load drops it."""
         if self._sess is not None:
-            self._sess.close()
-            self._sess = None
+            if keep_session:
+                self._sess.reset()
+            else:
+                self._sess.close()
+                self._sess = None
 
     def _run_batch(self, vals):
         """Values of coalesced requests -> [(has_output, value)] in order: on
         the one persistent instance as sequential calls (stateful), or as
         independent lanes (stateless); one executor launch either way."""
-        with self._lock:
-            if self.stateful:
-                return [(h, o) for h, o, _ in self._run_stateful(vals)]
+        if self.stateful:
+            return [(h, o) for h, o, _ in self._run_stateful(vals)]
+        with self._exec:
             r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
                                              stack_cap=self.stack_cap, devices=self.devices, steps=False)
         return [(bool(int(st) & N.MK_ST_HAS_OUTPUT), int(o)) for o, st in zip(r.out.tolist(), r.status.tolist())]
 
     def _run_stateful(self, vals):
         """Sequential /compute calls on the one instance -> [(has_output,
-        value, status)].  Caller holds self._lock.  A call that spends its
-        budget slice stays open (the reference's nodes never give up,
-        program.go:80-92): it is resumed until it has its output, closes, or
-        ``call_timeout`` passes (then 504, and the call is abandoned: the
-        instance lives on).  The burst's later calls, which did not run
-        behind it (MK_ST_CALL_OPEN), go in the next launch."""
-        sess = self.session()
+        value, status)].  A call that spends its budget slice stays open (the
+        reference's nodes never give up, program.go:80-92): it is resumed
+        until it has its output, closes, or the burst's ``call_timeout``
+        passes (then 504, and the call is abandoned: the instance lives on).
+        /reset, /pause and /load end the resuming at the next slice; the
+        burst's calls that did not run answer no output (MK_ST_BUDGET).  The
+        burst's later calls, which did not run behind an open call
+        (MK_ST_CALL_OPEN), go in the next launch."""
+        deadline = None if self.call_timeout is None else time.monotonic() + self.call_timeout
         res: list = []
-        while len(res) < len(vals):
-            r = sess.compute_seq(np.asarray(vals[len(res):], dtype=np.int64), steps=False, busy_ok=True)
-            for o, st in zip(r.out.tolist(), r.status.tolist()):
-                reason = st & N.MK_ST_REASON_MASK
-                if st & N.MK_ST_HAS_OUTPUT:
-                    res.append((True, o, st))
-                elif reason == N.MK_ST_BUDGET:
-                    res.append(self._finish_open_call(sess))
-                    break
-                elif reason == N.MK_ST_CALL_OPEN:  # left open before this burst
-                    sess.cancel()
-                    break
-                else:  # quiescent (the call closed, the instance lives on) or stack overflow
-                    res.append((False, 0, st))
+        with self._burst:
+            epoch = self._epoch
+            while len(res) < len(vals):
+                with self._exec:
+                    if self._epoch != epoch:
+                        break
+                    sess = self.session()
+                    r = sess.compute_seq(np.asarray(vals[len(res):], dtype=np.int64), steps=False, busy_ok=True)
+                for o, st in zip(r.out.tolist(), r.status.tolist()):
+                    reason = st & N.MK_ST_REASON_MASK
+                    if st & N.MK_ST_HAS_OUTPUT:
+                        res.append((True, o, st))
+                    elif reason == N.MK_ST_BUDGET:
+                        res.append(self._finish_open_call(sess, epoch, deadline))
+                        break
+                    elif reason == N.MK_ST_CALL_OPEN:  # left open before this burst
+                        with self._exec:
+                            if self._sess is sess:
+                                sess.cancel()
+                        break
+                    else:  # quiescent (the call closed, the instance lives on) or stack overflow
+                        res.append((False, 0, st))
+        res += [(False, 0, N.MK_ST_BUDGET)] * (len(vals) - len(res))
         return res
 
-    def _finish_open_call(self, sess):
-        deadline = None if self.call_timeout is None else time.monotonic() + self.call_timeout
+    def _finish_open_call(self, sess, epoch, deadline):
         while True:
-            r = sess.resume(steps=False)
-            o, st = int(r.out[0]), int(r.status[0])
-            if st & N.MK_ST_HAS_OUTPUT:
-                return True, o, st
-            if (st & N.MK_ST_REASON_MASK) != N.MK_ST_BUDGET:
-                return False, 0, st
-            if deadline is not None and time.monotonic() >= deadline:
-                sess.cancel()
-                return False, 0, st
+            with self._exec:
+                if self._epoch != epoch or self._sess is not sess:
+                    if self._sess is sess:  # /pause: the instance stays, its open call goes
+                        sess.cancel()
+                    return False, 0, N.MK_ST_BUDGET
+                r = sess.resume(steps=False)
+                o, st = int(r.out[0]), int(r.status[0])
+                if st & N.MK_ST_HAS_OUTPUT:
+                    return True, o, st
+                if (st & N.MK_ST_REASON_MASK) != N.MK_ST_BUDGET:
+                    return False, 0, st
+                if deadline is not None and time.monotonic() >= deadline:
+                    sess.cancel()
+                    return False, 0, st
 
     def _call(self, v: int):
         """One /compute: (has_output, value)."""
@@ -323,6 +353,7 @@ class MasterNode:
             if e:
                 return http_error(f"error pausing network: {e}", 400)
             self.is_running = False
+            self._epoch += 1  # a call being resumed stops at its next slice (cancelled)
             if self.wire is not None:
                 self.wire.cancel()  # stopNode: blocked GetInput calls return errors (master.go:117-119, 251-260)
             return Response(200, "Success")
@@ -333,7 +364,10 @@ class MasterNode:
             if e:
                 return http_error(f"error resetting network: {e}", 400)
             self.is_running = False
-            self._drop_state()  # resetNode on every node and the master's channels (master.go:129-138)
+            self._epoch += 1
+            with self._exec:  # at most one launch in flight to wait for
+                # resetNode on every node and the master's channels (master.go:129-138)
+                self._drop_state(keep_session=True)
             if self.wire is not None:
                 self.wire.reset()
             return Response(200, "Success")
@@ -356,7 +390,9 @@ class MasterNode:
             # RPC then does (master.go:165-175: broadcast reset, stopNode,
             # resetNode): node state, stacks and the master's channels
             self.is_running = False
-            self._drop_state()
+            self._epoch += 1
+            with self._exec:
+                self._drop_state()
             if self.wire is not None:
                 self.wire.reset()
             if self.node_info[target].get("type") != "program":
@@ -366,9 +402,10 @@ class MasterNode:
             except TisParseError as ex:
                 return http_error(f"error loading program on node {target}: {ex}", 400)
             self.programs[target] = program
-            if self._net is not None:
-                self._net.close()
-                self._net = None
+            with self._exec:
+                if self._net is not None:
+                    self._net.close()
+                    self._net = None
             return Response(200, "Success")
 
     def _values(self, form, key="value"):
@@ -406,14 +443,14 @@ class MasterNode:
             return http_error("cannot parse form", 400)
         except (ValueError, TypeError, AttributeError):
             return http_error("cannot parse value", 400)
-        with self._lock:
-            if self.stateful:  # sequential /compute calls on the one instance
-                got = self._run_stateful(vals)
-                outs, sts = [g[1] for g in got], [g[2] for g in got]
-            else:
+        if self.stateful:  # sequential /compute calls on the one instance
+            got = self._run_stateful(vals)
+            outs, sts = [g[1] for g in got], [g[2] for g in got]
+        else:
+            with self._exec:
                 r = self.network().compute_batch(np.asarray(vals, dtype=np.int64), budget=self.budget,
                                                  stack_cap=self.stack_cap, devices=self.devices, steps=False)
-                outs, sts = r.out.tolist(), r.status.tolist()
+            outs, sts = r.out.tolist(), r.status.tolist()
         has = [(x & N.MK_ST_HAS_OUTPUT) != 0 for x in sts]
         out = {"values": [x if h else None for x, h in zip(outs, has)], "status": sts}
         return Response(200, json.dumps(out) + "\n", "application/json")

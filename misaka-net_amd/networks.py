@@ -58,13 +58,23 @@ def sample_network():
     ]
 
 
-def pipeline_program(k: int, nodes: int, depth: int) -> str:
+def pipeline_program(k: int, nodes: int, depth: int, observe: bool = False) -> str:
+    """Node k of the C4 pipeline.  The bench network (observe=False) maps a
+    node's input y to c*y + d with c = (3^depth - 1)/2, which is even: after
+    8 nodes c^8 = 0 mod 2^32, so its int32 output is the same for every
+    input and only the last nodes' stack contents reach it.  observe=True
+    keeps y in the node's own port R0 and adds it back at the end (c + 1 =
+    (3^depth + 1)/2, odd): every node's stack order then reaches the output
+    of every lane, which is what the full-size parity tests check."""
     me, stk = f"p{k}", f"s{k}"
     first = "IN ACC" if k == 0 else "MOV R0, ACC"
     last = "OUT ACC" if k == nodes - 1 else f"MOV ACC, p{k + 1}:R0"
+    keep = [f"MOV ACC, {me}:R0"] if observe else []  # y into the node's own (drained) R0
+    add = ["ADD R0"] if observe else []
     return "\n".join(
         [
             first,
+            *keep,
             "SAV",  # BAK = x
             f"MOV {depth}, ACC",
             "PL: SWP",  # ACC = x+i, BAK = counter
@@ -96,14 +106,15 @@ def pipeline_program(k: int, nodes: int, depth: int) -> str:
             "JGZ QL",
             "MOV R1, NIL",  # drain the counter port
             "SWP",
+            *add,
             last,
             "",
         ]
     )
 
 
-def pipeline_network(depth: int = 64, nodes: int = 8):
-    out = [NodeSpec(f"p{k}", "program", pipeline_program(k, nodes, depth)) for k in range(nodes)]
+def pipeline_network(depth: int = 64, nodes: int = 8, observe: bool = False):
+    out = [NodeSpec(f"p{k}", "program", pipeline_program(k, nodes, depth, observe)) for k in range(nodes)]
     out += [NodeSpec(f"s{k}", "stack") for k in range(nodes)]
     return out
 

@@ -39,8 +39,34 @@ def _worker(rank, world, port, q):
     stats = torch.tensor([int(sp.sum()), int(((st & 0x10) != 0).sum()), hi - lo, 0, 0, 0, 0, 0], dtype=torch.int64)
     mk.dist.reduce_counters(stats, dist)
     g = mk.dist.gather_outputs(torch.from_numpy(out), dist)
+    # bench.py's end-to-end leg, the code an N-GPU run executes: K steps of
+    # (fill this rank's shard, ordered gather of out + status to rank 0),
+    # timed as the max over ranks, then rank 0 checks the gathered batch
+    # against one evaluation over all global lanes
+    o_t, s_t = torch.zeros(hi - lo, dtype=torch.int32), torch.zeros(hi - lo, dtype=torch.uint8)
+    calls = []
+
+    def step():
+        calls.append(1)
+        o_t.copy_(torch.from_numpy(out))
+        s_t.copy_(torch.from_numpy(st))
+
+    secs, g_out, g_st = mk.dist.timed_gather(step, o_t, s_t, dist, 3)
+    verified = None
     if rank == 0:
-        q.put((stats.numpy().tolist(), g.numpy().tolist()))
+        def full():
+            xa = po.gen_inputs(SEED, world * LANES)
+            fo, fs, _ = po.OracleNet(mk.networks.sample_network()).compute_batch(xa)
+            return torch.from_numpy(fo), torch.from_numpy(fs)
+
+        verified = mk.dist.verify_gathered(g_out, g_st, full)
+        wrong = g_out.clone()
+        wrong[LANES] ^= 1  # a lane of rank 1's shard: a gather out of order or short would differ too
+        caught = not mk.dist.verify_gathered(wrong, g_st, full)
+    else:
+        assert g_out is None and g_st is None
+    if rank == 0:
+        q.put((stats.numpy().tolist(), g.numpy().tolist(), secs > 0 and len(calls) == 3, verified, caught))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -54,7 +80,7 @@ def test_two_rank_shard_reduce_gather():
     procs = [ctx.Process(target=_worker, args=(r, world, _port_holder[0], q)) for r in range(world)]
     for p in procs:
         p.start()
-    stats, gathered = q.get(timeout=120)
+    stats, gathered, timed, verified, caught = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -63,6 +89,7 @@ def test_two_rank_shard_reduce_gather():
     assert gathered == out.tolist()  # ordered: rank order == global lane order
     assert stats[0] == int(sp.sum()) and stats[2] == world * LANES
     assert stats[1] == int(((st & 0x10) != 0).sum())
+    assert timed and verified and caught  # misaka_net_amd.dist.timed_gather / verify_gathered (bench.py)
 
 
 _port_holder = [_port()]

@@ -430,41 +430,64 @@ def test_c5_full_size_properties(gpu, mode):
     assert stats[0] == int(sp.astype(np.int64).sum()) and stats[2] == n
 
 
-def test_c4_full_size_properties(gpu):
-    # the C4 d64 bench workload: 1,048,576 lanes; the pipeline's control flow
-    # does not depend on x (every lane retires the same count and outputs);
-    # a seeded slice bit-exact against the oracle
-    n = 1 << 20
-    nodes = mk.networks.pipeline_network(64)
-    out, st, sp, stats = _device_run(mk.Network(nodes), n)
-    sl = slice(n - 2048, n)
-    ref = oracle(nodes, po.gen_inputs(SEED, n)[sl])
-    assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
-    assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
+def _affine(nodes):
+    """(A, B) with out(x) = int32(A*x + B) for the pipeline networks: every
+    hop truncates to int32 and the control flow does not depend on x, so
+    the int32 output is affine in x mod 2^32 (stack.go:95-155,
+    intStack.go:20-38, program.go:284-311); A and B from two oracle lanes."""
+    f = oracle(nodes, np.array([0, 1], np.int64))[0].astype(np.int64)
+    return (int(f[1]) - int(f[0])) % 2**32, int(f[0]) % 2**32
 
 
-# The other two C4 bench workloads at their bench sizes, through the default
-# heavy kernel (d256: 193 shared slots, the first 160 in LDS and the rest in
-# the wave's HBM block; d1024: 961 shared slots in HBM, wave-blocked buffer
-# slots, four launches of at most 69,824 inputs whose slot blocks fit the
-# Infinity Cache -- tis_jit.h kJitSlotBytes): constant status and steps on
-# every lane (the pipeline's control flow does not depend on x), the
-# counters, and a tail slice bit-exact against the oracle
-# (stack.go:95-155, intStack.go:20-38).
-@pytest.mark.parametrize("depth,n,tail", [(256, 1 << 19, 2048), (1024, 1 << 18, 512)])
-def test_c4_deep_full_size_properties(gpu, depth, n, tail):
+def _assert_affine_every_lane(out, x, A, B):
+    want = ((A * (x.astype(np.int64) % 2**32) + B) % 2**32).astype(np.uint32).view(np.int32)
+    bad = np.nonzero(out != want)[0]
+    assert not bad.size, f"{bad.size} lanes off the affine map; lane {bad[0]}: x={x[bad[0]]} out={out[bad[0]]}"
+
+
+# The C4 bench workloads at their bench sizes: d64 (1,048,576 lanes), d256
+# (524,288; the default heavy kernel: 193 shared slots, the first 160 in LDS
+# and the rest in the wave's HBM block) and d1024 (262,144; 961 shared slots
+# in HBM, wave-blocked buffer slots, launches of at most 69,824 inputs whose
+# slot blocks fit the Infinity Cache -- tis_jit.h kJitSlotBytes).  Every
+# lane is checked exactly: status and steps equal the oracle's (the control
+# flow does not depend on x) and out equals the oracle's affine map.  The
+# bench network's map has A = 0 (networks.pipeline_program: its x
+# coefficient vanishes after 8 nodes), so its every-lane check sees the last
+# nodes' stacks; the observe variant below carries every node's.
+@pytest.mark.parametrize("depth,n", [(64, 1 << 20), (256, 1 << 19), (1024, 1 << 18)])
+def test_c4_full_size_every_lane(gpu, depth, n):
     nodes = mk.networks.pipeline_network(depth)
     net = mk.Network(nodes)
-    assert "shape=stream-heavy" in net.plan(), net.plan()
+    if depth > 64:
+        assert "shape=stream-heavy" in net.plan(), net.plan()
     out, st, sp, stats = _device_run(net, n)
-    sl = slice(n - tail, n)
-    ref = oracle(nodes, po.gen_inputs(SEED, n)[sl])
-    assert np.array_equal(out[sl], ref[0]) and np.array_equal(st[sl], ref[1]) and np.array_equal(sp[sl], ref[2])
+    x = po.gen_inputs(SEED, n)
+    A, B = _affine(nodes)
+    assert A == 0
+    _assert_affine_every_lane(out, x, A, B)
+    ref = oracle(nodes, x[-512:])
+    assert np.array_equal(out[-512:], ref[0]) and np.array_equal(sp[-512:], ref[2])
     assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
-    # every lane's output is a function of its own input only: equal inputs, equal outputs
-    xs = po.gen_inputs(SEED, n)
-    head = oracle(nodes, xs[:tail])
-    assert np.array_equal(out[:tail], head[0])
+
+
+# The same workloads with pipeline_network(observe=True): each node adds its
+# input back at the end, so the x coefficient is odd and a wrong pop order,
+# a lost push or a slot mix-up in any node changes every lane's output.
+@pytest.mark.parametrize("depth,n", [(64, 1 << 20), (256, 1 << 19), (1024, 1 << 18)])
+def test_c4_observe_full_size_every_lane(gpu, depth, n):
+    nodes = mk.networks.pipeline_network(depth, observe=True)
+    bench = mk.Network(mk.networks.pipeline_network(depth)).plan().split("shape=")[1].split()[0]
+    net = mk.Network(nodes)
+    assert net.plan().split("shape=")[1].split()[0] == bench, net.plan()  # the bench network's kernel shape
+    out, st, sp, stats = _device_run(net, n)
+    x = po.gen_inputs(SEED, n)
+    A, B = _affine(nodes)
+    assert A % 2 == 1
+    _assert_affine_every_lane(out, x, A, B)
+    ref = oracle(nodes, x[:512])
+    assert np.array_equal(out[:512], ref[0]) and np.array_equal(sp[:512], ref[2])
+    assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -109,6 +109,8 @@ def test_configs(tmp_path, machine):
         kind = 1 if name.startswith("c5") else 0
         cases.append((name, mk.networks.CONFIGS[name](), po.gen_inputs(SEED, 2000, kind=kind, mask=1023), {}))
     cases.append(("c4_d1024", mk.networks.pipeline_network(1024), po.gen_inputs(SEED, 40), {}))
+    for d in (64, 256):  # every node's stack order reaches the output (networks.pipeline_program)
+        cases.append((f"c4_observe_d{d}", mk.networks.pipeline_network(d, observe=True), po.gen_inputs(SEED, 200), {}))
     cases.append(("c5_all_trips", mk.networks.countdown_network(), np.arange(0, 1024, dtype=np.int64), {}))
     for b in (1, 11, 12, 13):
         cases.append((f"c2_budget{b}", mk.networks.example_network(), po.gen_inputs(SEED, 300), {"budget": b}))

@@ -345,6 +345,10 @@ class _OracleSession:
     def cancel(self):
         self.o.cancel()
 
+    def reset(self):
+        self.resets = getattr(self, "resets", 0) + 1
+        self.o.reset()
+
     def close(self):
         self.closed = True
 
@@ -393,6 +397,59 @@ def test_call_timeout_abandons_the_call():
     assert time.monotonic() - t0 >= 0.2
     assert _compute(m, 5) == (200, '{"value":5}\n')  # the abandoned call left its 0 with b
     assert m._sess.launches > 3
+
+
+def _spin_in_thread(m, x):
+    box = {}
+    t = threading.Thread(target=lambda: box.update(r=_compute(m, x)), daemon=True)
+    t.start()
+    time.sleep(0.15)  # the call is being resumed slice after slice
+    assert t.is_alive()
+    return t, box
+
+
+def test_reset_during_a_spinning_call_returns_at_once():
+    # a call being resumed holds the executor one slice at a
+    # time, so /reset does not wait for it; the call stops at its next slice
+    # (504) and the instance restarts from its initial state (kept compiled:
+    # mk_session_reset, not a new session)
+    m = _stateful(SPINNER, sess_budget=1000, call_timeout=None)
+    sess = m._sess
+    t, box = _spin_in_thread(m, 0)
+    t0 = time.monotonic()
+    assert m.handle("POST", "/reset").code == 200
+    assert time.monotonic() - t0 < 0.5
+    t.join(timeout=5)
+    assert not t.is_alive() and box["r"] == (504, "network produced no output\n")
+    assert m._sess is sess and sess.resets == 1 and not sess.closed
+    m.handle("POST", "/run")
+    assert _compute(m, 5) == (200, '{"value":5}\n')
+    # b's port is empty again after /reset: a zero goes in, a later 5 answers
+    assert m._run_batch([7]) == [(True, 7)]
+
+
+def test_pause_during_a_spinning_call_cancels_it_and_keeps_state():
+    m = _stateful(SPINNER, sess_budget=1000, call_timeout=None)
+    t, box = _spin_in_thread(m, 0)
+    t0 = time.monotonic()
+    assert m.handle("POST", "/pause").code == 200
+    assert time.monotonic() - t0 < 0.5
+    t.join(timeout=5)
+    assert box["r"] == (504, "network produced no output\n")
+    m.handle("POST", "/run")
+    assert _compute(m, 5) == (200, '{"value":5}\n')  # the instance kept its state
+    assert getattr(m._sess, "resets", 0) == 0
+
+
+def test_one_deadline_for_the_whole_burst():
+    # three calls that never answer: the burst ends at call_timeout, not
+    # three times it
+    m = _stateful(SPINNER, sess_budget=1000, call_timeout=0.3)
+    t0 = time.monotonic()
+    got = m._run_batch([0, 0, 0])
+    dt = time.monotonic() - t0
+    assert got == [(False, 0)] * 3
+    assert 0.3 <= dt < 0.6, dt
 
 
 @pytest.mark.gpu

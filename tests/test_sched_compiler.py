@@ -40,6 +40,11 @@ def test_deep_pipeline_d1024():
     same(mk.networks.pipeline_network(1024), po.gen_inputs(SEED, 40))
 
 
+@pytest.mark.parametrize("depth", [64, 1024])
+def test_observe_pipeline(depth):
+    same(mk.networks.pipeline_network(depth, observe=True), po.gen_inputs(SEED, 40))
+
+
 @pytest.mark.parametrize("budget", [1, 5, 11, 12, 13, 100])
 def test_budget_boundaries(budget):
     same(mk.networks.example_network(), po.gen_inputs(SEED, 64), budget=budget)
