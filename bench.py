@@ -40,7 +40,19 @@ HBM_PEAK = 8.0e12
 L2_PEAK = 34.5e12  # aggregate XCD L2 bandwidth, MI355X_MICROARCH.md section L2
 # LDS (MI355X_MICROARCH.md section LDS): one LDS array per CU, 256 CUs at 2.4 GHz
 LDS_CUS, LDS_CLOCK = 256, 2.4e9
-LDS_PEAK = 150e12  # aggregate ds_read_b64/b128 bytes/s, the guide's LDS section
+# 4-byte stack slots move by ds_write_b32 / ds_read_b32, whose rates the guide
+# gives per CU: 64 B/clk for ds_write_b32 (4 cycles per wave-instruction: the
+# address and data transfer) and 128 B/clk for ds_read_b32 (2 LDS cycles).  A
+# slot is written once (PUSH) and read once (POP): half the LDS-resident
+# bytes at each rate.  (Round 3 priced them at 150 TB/s, the guide's
+# ds_read_b64/b128 figure: 2-4x too fast for 4-byte slots.)
+LDS_WRITE_B32 = 64 * LDS_CUS * LDS_CLOCK  # 39.3 TB/s
+LDS_READ_B32 = 128 * LDS_CUS * LDS_CLOCK  # 78.6 TB/s
+
+
+def lds_slot_seconds(nbytes):
+    """Lower bound on the LDS time of `nbytes` of slot traffic, half pushes, half pops."""
+    return nbytes / 2 / LDS_WRITE_B32 + nbytes / 2 / LDS_READ_B32
 
 WORKLOADS = {
     # name: (workload, network factory, lanes per GPU, generator kind, mask)
@@ -537,7 +549,8 @@ def main():
     # I/O is known to cross HBM: the slot bytes are priced at the L2 peak, a
     # lower bound on the memory time, so `frac` stays a bound (<= 1).
     fabric = min(traffic, bytes_per_launch) if traffic else io_bytes
-    t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / (LDS_PEAK if lds_split else L2_PEAK)
+    t_mem = fabric / HBM_PEAK + (lds_slot_seconds(bytes_per_launch - fabric) if lds_split
+                                 else (bytes_per_launch - fabric) / L2_PEAK)
     hbm = {
         "bound": "hbm",
         "achieved": hbm_achieved / 1e9,
@@ -548,7 +561,8 @@ def main():
         "bytes_per_lane": bytes_per_launch // lanes,
         "bytes_per_launch": bytes_per_launch,
         "launch_us": launch_max * 1e6,
-        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + LDS-resident bytes / 150 TB/s)"
+        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + LDS-resident bytes, half at ds_write_b32's "
+                  "39.3 TB/s and half at ds_read_b32's 78.6 TB/s)"
                   if traffic and lds_split else
                   "peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
                   if traffic and bytes_per_launch > fabric * 1.001 else
@@ -618,6 +632,25 @@ def main():
                    "launch_us": launch_max * 1e6, "counter_source": prof.get("source")}
         else:
             lds = {"bound": "lds", "frac": None, "model": "no PMC profile of this kernel: LDS work not measured"}
+    # C4: how much of the stack traffic the kernel actually executes (VERDICT
+    # r03 item 5).  Slot instructions = LDS wave-instructions + the vector
+    # memory instructions beyond the lanes' I/O (one input load, the out and
+    # status stores per wave), times 64 lanes, per retired PUSH/POP.  Near 1:
+    # every push and pop is a memory operation (d256, d1024); far below 1:
+    # the compiler forwarded pushes to pops in registers (d64, straight-line
+    # code with static slot indices) -- that config then measures the
+    # folded program, not stack traffic.
+    stack = None
+    if STACK_OPS_PER_LANE.get(args.config) and args.config.startswith("c4"):
+        pp = STACK_OPS_PER_LANE[args.config] * lanes
+        lsq, ssq = prof.get("lds", {}), prof.get("sq", {})
+        stack = {"push_pop_per_launch": pp, "stack_ops_executed_per_push_pop": None,
+                 "model": "(SQ_INSTS_LDS + SQ_INSTS_VMEM_RD + SQ_INSTS_VMEM_WR - 3 x waves) x 64 / retired PUSH+POP"}
+        if lsq.get("SQ_INSTS_LDS") is not None and ssq.get("SQ_INSTS_VMEM_RD") is not None:
+            waves = lanes / 64
+            slot_vmem = max(0.0, ssq["SQ_INSTS_VMEM_RD"] + ssq.get("SQ_INSTS_VMEM_WR", 0.0) - 3 * waves)
+            stack["stack_ops_executed_per_push_pop"] = (lsq["SQ_INSTS_LDS"] + slot_vmem) * 64 / pp
+            stack["counter_source"] = prof.get("source")
     # The dominant kernel's roofline is the tightest bound: the byte stream
     # for short networks (C2, C3), integer issue for long ones, LDS for
     # stacks kept there.
@@ -668,6 +701,8 @@ def main():
             "roofline_lds": lds,
             "cpu_baseline": cpu,
         }
+        if stack is not None:
+            rec["stack"] = stack
         if e2e is not None:
             rec["end_to_end"] = e2e
         if host_io is not None:

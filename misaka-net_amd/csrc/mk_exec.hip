@@ -2674,6 +2674,10 @@ int ensure_jit_device(SchedCache *sc, int d)
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, sc->jit.block, 0) != hipSuccess ||
         jd.per_cu < 1)
         jd.per_cu = 1;
+    if (const char *e = std::getenv("MK_JIT_PER_CU"); e && *e) // diagnostics: resident blocks per CU of the grid
+        jd.per_cu = std::max(1, std::min(jd.per_cu, std::atoi(e)));
+    if (std::getenv("MK_JIT_SHOW_GRID"))
+        fprintf(stderr, "mk: native kernel on device %d: %d blocks of %d per CU\n", d, jd.per_cu, sc->jit.block);
     return MK_OK;
 }
 
@@ -3110,10 +3114,14 @@ int session_native(mk_session *s)
     s->p.nsb = s->nsb;
     s->p.hand_call = s->hand_call;
     s->p.sflags = s->sflags;
-    char line[256];
+    // registers a launch loads and stores per instance (mk_sess_load's lines):
+    // with sb, the state bytes of the sessions' byte model (tools/sess_roofline.py)
+    size_t live_regs = 0;
+    for (size_t at = src.find("on ? regs["); at != std::string::npos; at = src.find("on ? regs[", at + 1)) ++live_regs;
+    char line[320];
     snprintf(line, sizeof line, "tier=native superblocks=%u regs=%u slots=%u words=%zu source=%zuB kernel=%016llx "
-             "compile=%.2fs rtc=%s", P.nsb, P.nregs, P.nslots, P.code.size(), src.size(),
-             (unsigned long long)src_hash(src), secs, from.c_str());
+             "compile=%.2fs rtc=%s state_regs=%zu", P.nsb, P.nregs, P.nslots, P.code.size(), src.size(),
+             (unsigned long long)src_hash(src), secs, from.c_str(), live_regs);
     s->plan = line;
     return MK_OK;
 }

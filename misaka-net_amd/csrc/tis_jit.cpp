@@ -2070,6 +2070,134 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 }
 )";
 
+// Kernel of the machine shape with lanes grouped by value inside each
+// WAVE's share, and no block barriers (MK_JIT_TS_WAVE=1).  Every wave owns a
+// contiguous run of whole 64-input chunks (the same count +-1 for every
+// wave of the grid) and takes it in tiles of at most MK_WS_T inputs:
+//   1. loads them (lane-strided, coalesced), buckets them by value in its
+//      own LDS region: wave min / max, 64 buckets of equal width (a power of
+//      two), a histogram, its prefix sum (one bucket per lane, shuffles) and a
+//      scatter -- a counting sort whose order inside a bucket does not matter;
+//   2. runs them in sorted order, 64 at a time, every chunk by generations;
+//   3. writes each chunk's results straight to their input positions.
+// Nothing waits for another wave: the block-tile kernel's barriers left a
+// wave parked while the slowest wave of its block finished (r04l: 38% of C5's
+// wave cycles in SQ_WAIT_ANY).
+static const char *const kMachineWaveSortKernel = R"(
+#define MK_WS_T (64u * MK_WS_R)
+#define MK_WS_NB 64u
+MK_FN void mk_ws_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
+{
+    __shared__ int32_t s_key[4][MK_WS_T];
+    __shared__ uint16_t s_pos[4][MK_WS_T];
+    __shared__ uint32_t s_cnt[4][MK_WS_NB];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
+    const uint32_t pol = MK_POLICY;
+    int32_t *const key = s_key[wave];
+    uint16_t *const pos = s_pos[wave];
+    uint32_t *const cnt = s_cnt[wave];
+    uint64_t c_steps = 0u;
+    uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
+    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+    const uint64_t gw = (uint64_t)blockIdx.x * 4u + wave, nw = (uint64_t)gridDim.x * 4u;
+    const uint64_t nch = (p.n + 63u) / 64u;
+    const uint64_t c0 = nch * gw / nw, c1 = nch * (gw + 1u) / nw;
+    const uint64_t end = c1 * 64u < p.n ? c1 * 64u : p.n;
+    for (uint64_t base = c0 * 64u; base < end; base += MK_WS_T) {
+        const uint32_t m = end - base < MK_WS_T ? (uint32_t)(end - base) : MK_WS_T;
+        // 1. inputs base + 64 k + lane, their range
+        int32_t v[MK_WS_R];
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u; // biased: signed order as unsigned
+        for (uint32_t k = 0; k < MK_WS_R; ++k) {
+            const uint32_t i = 64u * k + lane;
+            v[k] = i < m ? sched_input(p, base + i) : 0;
+            const uint32_t b = (uint32_t)v[k] ^ 0x80000000u;
+            if (i < m) {
+                lo = b < lo ? b : lo;
+                hi = b > hi ? b : hi;
+            }
+        }
+        lo = MK_WAVE_MIN(lo);
+        hi = MK_WAVE_MAX(hi);
+        const uint32_t span = hi - lo;
+        const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
+        const uint32_t sh = bits > 6u ? bits - 6u : 0u;
+        cnt[lane] = 0u;
+        mk_ws_sync();
+        for (uint32_t k = 0; k < MK_WS_R; ++k) // (buckets recomputed below: fewer registers)
+            if (64u * k + lane < m) atomicAdd(&cnt[(((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh], 1u);
+        mk_ws_sync();
+        {   // exclusive prefix sum over the 64 buckets (lane l owns bucket l)
+            const uint32_t c = cnt[lane];
+            uint32_t x = c;
+            for (uint32_t o = 1u; o < 64u; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if (lane >= o) x += y;
+            }
+            mk_ws_sync();
+            cnt[lane] = x - c;
+        }
+        mk_ws_sync();
+        for (uint32_t k = 0; k < MK_WS_R; ++k) {
+            const uint32_t i = 64u * k + lane;
+            if (i >= m) continue;
+            const uint32_t d = atomicAdd(&cnt[(((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh], 1u);
+            key[d] = v[k];
+            pos[d] = (uint16_t)i;
+        }
+        mk_ws_sync();
+        // 2. the sorted lanes, 64 per chunk; 3. results to their input positions
+        const uint32_t nc = (m + 63u) / 64u;
+        for (uint32_t c = 0; c < nc; ++c) {
+            const uint32_t j = c * 64u + lane;
+            const bool live = j < m;
+            MkLane L;
+            mk_init(L, live ? key[j] : 0);
+            const uint32_t at = live ? pos[j] : 0u;
+            if (!live) L.sb = MK_SB_IDLE;
+            for (;;) {
+                const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
+                if (!actb) break;
+                const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
+                const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
+                if (L.sb == u) mk_run(u, L, p.budget, slots, p.lanes, pol, smax);
+            }
+            if (live) {
+                p.out[base + at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+                p.status[base + at] = (uint8_t)L.st;
+                if (p.steps) p.steps[base + at] = L.steps;
+            }
+            const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
+            c_steps += (uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps & 0xffffu) : 0u)) +
+                       ((uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps >> 16) : 0u)) << 16);
+            c_out += (uint32_t)__popcll(__ballot(live && (L.st & MK_ST_HAS_OUTPUT)));
+            c_done += (uint32_t)__popcll(__ballot(live));
+            c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
+            c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
+            c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
+            c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
+        }
+        mk_ws_sync(); // the next tile reuses the wave's LDS
+    }
+    if (p.partials && lane == 0u) { // this wave's row (write_partials' layout)
+        unsigned long long *q = p.partials + (gid >> 6) * 8u;
+        q[0] += c_steps;
+        q[1] += c_out;
+        q[2] += c_done;
+        q[3] += c_qu;
+        q[4] += c_bu;
+        q[5] += c_ov;
+        q[6] += c_os;
+    }
+}
+)";
+
 JitLimits JitLimits::from_env()
 {
     JitLimits l;
@@ -2115,6 +2243,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     num("MK_JIT_SAT_DEC", l.sat_dec);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
+    flag("MK_JIT_TS_WAVE", l.ts_wave);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
     flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
@@ -2135,7 +2264,7 @@ std::string JitLimits::key() const
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)sat_dec, (int)ts_dyn,
              (int)tune_regs,
              lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad);
-    return b;
+    return ts_wave ? std::string(b) + ",tswave=1" : std::string(b);
 }
 
 // Kernel of the machine shape with lane compaction.  One wave per block,
@@ -2463,6 +2592,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
+    if (lim.ts_wave) e.line("#define MK_WS_R 12u"); // kMachineWaveSortKernel: a wave's tile, inputs per lane
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks
@@ -2616,7 +2746,8 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     Emitter e;
     e.s = module_prelude(shape, lim, pool, lane_src.find("MK_SAT") != std::string::npos);
     e.s += lane_src;
-    const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel : kMachineKernel;
+    const char *mk = lim.tile_sort && !lim.order ? (lim.ts_wave ? kMachineWaveSortKernel : kMachineSortKernel)
+                                                 : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
     else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;
     e.s += shape == JIT_MACHINE ? mk : heavy ? kStreamKernelHeavy : kStreamKernel;

@@ -117,6 +117,9 @@ struct JitLimits {
     // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
     // order.
     bool ts_dyn = false;
+    // Its variant without block barriers: each wave sorts and runs its own
+    // contiguous share (MK_JIT_TS_WAVE=1, kMachineWaveSortKernel).
+    bool ts_wave = false;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the

@@ -10,11 +10,14 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 for kv in "$@"; do export "$kv"; done
 STALL="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"
-echo "[pmc-stall] $(date +%T) $CFG"
-timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $STALL --output-format csv -d "$OUT/STALL" -o p -- \
-  python3 bench.py --config $CFG --steps 6 --warmup 1 --no-cpu-baseline > "$OUT/STALL.log" 2>&1 \
-  || { echo "[pmc-stall] failed"; tail -5 "$OUT/STALL.log"; exit 1; }
-python3 - "$OUT/STALL" <<'PY'
+# second pass: instruction mix and the LDS-issue share of the issue stalls
+STALL2="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"
+for pass in STALL STALL2; do
+echo "[pmc-stall] $(date +%T) $CFG $pass"
+timeout -s KILL 150 rocprofv3 --kernel-trace --pmc ${!pass} --output-format csv -d "$OUT/$pass" -o p -- \
+  python3 bench.py --config $CFG --steps 6 --warmup 1 --no-cpu-baseline > "$OUT/$pass.log" 2>&1 \
+  || { echo "[pmc-stall] failed"; tail -5 "$OUT/$pass.log"; exit 1; }
+python3 - "$OUT/$pass" <<'PY'
 import collections, csv, glob, sys
 rows = collections.defaultdict(lambda: collections.defaultdict(float))
 for p in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
@@ -25,4 +28,5 @@ ids = sorted(rows)[2:]
 for c in sorted(rows[ids[0]]):
     print(f"{c:24s} {sum(rows[i][c] for i in ids) / len(ids):16.0f}")
 PY
+done
 echo "[pmc-stall] done"
