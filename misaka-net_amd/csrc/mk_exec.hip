@@ -933,6 +933,20 @@ __global__ void __launch_bounds__(B) tis_sched_tile(const DOp *__restrict__ code
 // result and the instance lives on; a stack overflow ends the session.
 // Ports are staged in LDS for the call; stack entries stay in HBM.
 // ------------------------------------------------------------------------
+struct SessImport {
+    uint64_t n;
+    int nprog, nstack;
+    uint32_t *nsb;
+    uint32_t *sflags;   // SessParams::sflags (written here)
+    uint32_t epoch;     // this launch (the native kernel stores it into sflags[0] at a hand-off)
+    const uint32_t *hand_sb, *hand_steps;
+    const int64_t *regs;  // [register][n]
+    const int32_t *slots; // [slot][n]
+    const SessMapHdr *hdr;
+    const SessSrcDev *rec;
+    const int64_t *dyn_base;
+};
+
 struct SessParams {
     uint32_t base[MK_MAX_PROGRAM_NODES];
     uint32_t len[MK_MAX_PROGRAM_NODES];
@@ -966,16 +980,64 @@ struct SessParams {
     uint32_t resume;    // continue each session's parked call (in ignored)
     // native sessions (tis_jit.h mk_sess_exec): the interpreter runs only the
     // sessions marked MK_SS_T1 here (null: all).  One handed off in this
-    // launch (io bit 8, set by tis_session_import) starts at its call
+    // launch (io bit 8, set by sess_import_one) starts at its call
     // hand_call[i], resumed, its step count that of the native slice, at
     // round position io bits 9-13 with io bit 14 "something changed".
     const uint32_t *nsb;       // [n]
     const uint32_t *hand_call; // [n]
     // [0] launch epoch of the last hand-off, [1] sessions the interpreter
-    // holds (tis_session_import counts them): with none and no resume this
+    // holds (sess_import_one counts them): with none and no resume this
     // kernel has nothing to do
     const uint32_t *sflags;
+    // the hand-off import, done by this kernel before it runs (one launch
+    // fewer per call than round 3's separate import kernel)
+    uint32_t fuse_import;
+    SessImport imp;
 };
+
+struct SessImportOut {
+    const SessParams &p;
+    uint64_t i, n;
+    uint32_t io = 0;
+    __device__ void acc(int k, int64_t v) { p.acc[(uint64_t)k * n + i] = v; }
+    __device__ void bak(int k, int64_t v) { p.bak[(uint64_t)k * n + i] = v; }
+    __device__ void ip(int k, int32_t v) { p.ip[(uint64_t)k * n + i] = v; }
+    __device__ void pendv(int k, int32_t v) { p.pendv[(uint64_t)k * n + i] = v; }
+    __device__ void port(int q, int32_t v) { p.port[(uint64_t)q * n + i] = v; }
+    __device__ void pfull(uint64_t x) { p.pfull[i] = x; }
+    __device__ void bits(uint32_t pend, uint32_t hung) { p.bits[i] = (pend & 0xffffu) | (hung << 16); }
+    __device__ void chans(bool in_full, bool out_full, int32_t iv, int32_t ov)
+    {
+        io |= (in_full ? 1u : 0u) | (out_full ? 2u : 0u);
+        p.in_val[i] = iv;
+        p.out_val[i] = ov;
+    }
+    __device__ void depth(int s, uint32_t d) { p.sdepth[(uint64_t)s * n + i] = (int32_t)d; }
+    __device__ void entry(int s, uint32_t d, int32_t v) { p.stk[((uint64_t)s * p.stack_cap + d) * n + i] = v; }
+    __device__ void call(bool dep, int32_t pin, int pos, bool changed)
+    {
+        io |= 8u | 0x100u | (dep ? 0u : 4u) | ((uint32_t)pos << 9) | (changed ? 0x4000u : 0u);
+        p.pin[i] = pin;
+    }
+};
+
+// One session's hand-off import (the native kernel's state at a HANDOFF into
+// the interpreter's arrays, sess_convert.h), done by the
+// interpreter kernel itself first (SessParams::fuse_import).
+__device__ __forceinline__ void sess_import_one(const SessImport &q, const SessParams &p, uint64_t gid)
+{
+    if (gid >= q.n || q.nsb[gid] != kSessHand) return;
+    const SessMapHdr h = q.hdr[q.hand_sb[gid]];
+    const uint64_t n = q.n;
+    auto reg = [&](uint32_t r) { return q.regs[(uint64_t)r * n + gid]; };
+    auto slot = [&](uint32_t s) { return q.slots[(uint64_t)s * n + gid]; };
+    SessImportOut o{p, gid, n};
+    sess_convert(q.nprog, q.nstack, h, q.rec + h.off, q.dyn_base, reg, slot, o);
+    p.io[gid] = o.io;
+    p.csteps[gid] = q.hand_steps[gid];
+    q.nsb[gid] = kSessT1;
+    atomicAdd(&q.sflags[1], 1u);
+}
 
 template <int NMAX>
 __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ code, SessParams p)
@@ -987,7 +1049,13 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     const uint64_t n = p.n;
     int32_t *const port = lds;                     // [nprog*4][B]
     int32_t *const sdepth = lds + p.nprog * 4 * B; // [nstack][B]
-    if (p.nsb && !p.resume && p.sflags[1] == 0u) return; // every session is the native tier's
+    if (p.fuse_import) {
+        const bool handed = p.imp.sflags[0] == p.imp.epoch; // something was handed off in this launch
+        if (!handed && !p.resume && p.sflags[1] == 0u) return; // every session is the native tier's
+        if (handed) sess_import_one(p.imp, p, gid);
+    } else if (p.nsb && !p.resume && p.sflags[1] == 0u) {
+        return; // every session is the native tier's
+    }
     const bool live = gid < n && (!p.nsb || p.nsb[gid] == kSessT1);
 
     int64_t acc[NMAX], bak[NMAX];
@@ -1294,62 +1362,8 @@ __global__ void __launch_bounds__(kBlock) tis_session_cancel(uint32_t *io, uint6
 // map of that superblock's entry (tis_sched.h SessMapHdr, from the schedule
 // compiler) with the lane's registers and stack slots, in the interpreter's
 // arrays (sess_convert.h), the call open and continuing its slice.
-struct SessImport {
-    uint64_t n;
-    int nprog, nstack;
-    uint32_t *nsb;
-    uint32_t *sflags;   // SessParams::sflags (written here)
-    uint32_t epoch;     // this launch (the native kernel stores it into sflags[0] at a hand-off)
-    const uint32_t *hand_sb, *hand_steps;
-    const int64_t *regs;  // [register][n]
-    const int32_t *slots; // [slot][n]
-    const SessMapHdr *hdr;
-    const SessSrcDev *rec;
-    const int64_t *dyn_base;
-};
 
-struct SessImportOut {
-    const SessParams &p;
-    uint64_t i, n;
-    uint32_t io = 0;
-    __device__ void acc(int k, int64_t v) { p.acc[(uint64_t)k * n + i] = v; }
-    __device__ void bak(int k, int64_t v) { p.bak[(uint64_t)k * n + i] = v; }
-    __device__ void ip(int k, int32_t v) { p.ip[(uint64_t)k * n + i] = v; }
-    __device__ void pendv(int k, int32_t v) { p.pendv[(uint64_t)k * n + i] = v; }
-    __device__ void port(int q, int32_t v) { p.port[(uint64_t)q * n + i] = v; }
-    __device__ void pfull(uint64_t x) { p.pfull[i] = x; }
-    __device__ void bits(uint32_t pend, uint32_t hung) { p.bits[i] = (pend & 0xffffu) | (hung << 16); }
-    __device__ void chans(bool in_full, bool out_full, int32_t iv, int32_t ov)
-    {
-        io |= (in_full ? 1u : 0u) | (out_full ? 2u : 0u);
-        p.in_val[i] = iv;
-        p.out_val[i] = ov;
-    }
-    __device__ void depth(int s, uint32_t d) { p.sdepth[(uint64_t)s * n + i] = (int32_t)d; }
-    __device__ void entry(int s, uint32_t d, int32_t v) { p.stk[((uint64_t)s * p.stack_cap + d) * n + i] = v; }
-    __device__ void call(bool dep, int32_t pin, int pos, bool changed)
-    {
-        io |= 8u | 0x100u | (dep ? 0u : 4u) | ((uint32_t)pos << 9) | (changed ? 0x4000u : 0u);
-        p.pin[i] = pin;
-    }
-};
 
-__global__ void __launch_bounds__(kBlock) tis_session_import(SessImport q, SessParams p)
-{
-    if (q.sflags[0] != q.epoch) return; // nothing was handed off in this launch
-    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (gid >= q.n || q.nsb[gid] != kSessHand) return;
-    const SessMapHdr h = q.hdr[q.hand_sb[gid]];
-    const uint64_t n = q.n;
-    auto reg = [&](uint32_t r) { return q.regs[(uint64_t)r * n + gid]; };
-    auto slot = [&](uint32_t s) { return q.slots[(uint64_t)s * n + gid]; };
-    SessImportOut o{p, gid, n};
-    sess_convert(q.nprog, q.nstack, h, q.rec + h.off, q.dyn_base, reg, slot, o);
-    p.io[gid] = o.io;
-    p.csteps[gid] = q.hand_steps[gid];
-    q.nsb[gid] = kSessT1;
-    atomicAdd(&q.sflags[1], 1u);
-}
 
 // ---- input order for the machine shape (tier 3) -----------------------------
 // A wave of the machine-shape kernel runs 64 lanes together and each
@@ -3023,15 +3037,11 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
         if (hipModuleLaunchKernel(s->fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr) !=
             hipSuccess)
             return MK_EDEVICE;
-        // 2. calls it handed off become interpreter sessions
-        SessImport q{s->n, s->nprog, s->nstack, s->nsb, s->sflags, s->epoch, s->hand_sb, s->hand_steps, s->regs,
-                     s->slots, s->hdr, s->rec, s->dyn_base};
-        void *iargs[] = {(void *)&q, (void *)&p};
-        if (hipLaunchKernel(reinterpret_cast<void *>(&tis_session_import), dim3((unsigned)blocks), dim3(kBlock), iargs,
-                            0, stream) != hipSuccess) {
-            s->broken = true;
-            return MK_EDEVICE;
-        }
+        // 2. calls it handed off become interpreter sessions: imported by
+        // the interpreter kernel itself, thread by thread, before it runs
+        p.fuse_import = 1u;
+        p.imp = SessImport{s->n, s->nprog, s->nstack, s->nsb, s->sflags, s->epoch, s->hand_sb, s->hand_steps,
+                           s->regs, s->slots, s->hdr, s->rec, s->dyn_base};
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};

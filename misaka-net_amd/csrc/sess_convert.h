@@ -3,7 +3,7 @@
 // terms: instruction pointers, ACC / BAK, ports, pending sends, stacks, the
 // master's inChan / outChan and the open call (its input, whether it is
 // deposited, where the round stands).  One restatement for the GPU import
-// kernel (mk_exec.hip tis_session_import) and the host model's CPU tests
+// kernel (mk_exec.hip sess_import_one) and the host model's CPU tests
 // (sched_check.cpp): the map comes from the schedule compiler
 // (tis_sched.h SessMapHdr / SessSrcDev), the data from the lane's
 // registers and stack slots.

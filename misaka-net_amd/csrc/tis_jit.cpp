@@ -1429,7 +1429,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         e.line("#define MK_SS_HANDOFF 0xFEu");     // L.st of a lane handed to the interpreter
         e.line("#define MK_SS_DEAD 0xFFFFFFF0u");  // session ended (stack overflow)
         e.line("#define MK_SS_T1 0xFFFFFFF1u");    // the interpreter holds the session
-        e.line("#define MK_SS_HAND 0xFFFFFFF2u");  // handed off in this launch (tis_session_import converts it)
+        e.line("#define MK_SS_HAND 0xFFFFFFF2u");  // handed off in this launch (the interpreter kernel imports it, sess_import_one)
     }
     {
         uint32_t used = 0;
@@ -1715,6 +1715,49 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
 // loads the next tile's 16 bytes before running the current 4 lanes one
 // after another, and writes 16 B of out + 4 B of status per tile (+16 B of
 // steps on request).  Counters fold per wave (stats_reduce).
+// Counters of the stream kernels (the per-wave rows of write_partials /
+// add_partials): the step sum per thread, the statuses by ballots in
+// wave-uniform registers -- a lane costs a compare per status kind instead of
+// count_lane's seven 64-bit adds, which made the counting launches of the
+// light kernel VALU-bound (C3: 16.8 vs 12.2 us per launch, r04i).  Called in
+// wave-uniform control flow, once per lane slot (`live`: the slot holds an
+// input), so the ballots see every lane of the wave.
+static const char *const kStreamCount = R"(
+struct MkCount {
+    unsigned long long steps;                  // per thread
+    uint32_t out, done, qu, bu, ov, os;        // wave-uniform
+};
+__device__ __forceinline__ void mk_count(MkCount &c, bool live, uint32_t steps, uint32_t st)
+{
+    const uint32_t r = live ? (st & MK_ST_REASON_MASK) : 0u;
+    c.steps += live ? steps : 0u;
+    c.done += (uint32_t)__popcll(__ballot(live));
+    c.out += (uint32_t)__popcll(__ballot(live && (st & MK_ST_HAS_OUTPUT)));
+    c.qu += (uint32_t)__popcll(__ballot(r == MK_ST_QUIESCENT));
+    if (__ballot(live && r != MK_ST_QUIESCENT)) { // the other ends, counted where they occur
+        c.bu += (uint32_t)__popcll(__ballot(r == MK_ST_BUDGET));
+        c.ov += (uint32_t)__popcll(__ballot(r == MK_ST_STACK_OVERFLOW));
+        c.os += (uint32_t)__popcll(__ballot(r == MK_ST_OUTPUT_STOP));
+    }
+}
+// The wave's row: its own (gid >> 6), or row (gid >> 6) % rows added atomically.
+__device__ __forceinline__ void mk_count_store(unsigned long long *partials, uint32_t rows, uint64_t gid,
+                                               const MkCount &c)
+{
+    const unsigned long long s = wave_sum(c.steps);
+    if ((gid & 63) != 0) return;
+    const unsigned long long v[7] = {s, c.out, c.done, c.qu, c.bu, c.ov, c.os};
+    if (!rows) {
+        unsigned long long *q = partials + (gid >> 6) * 8;
+        for (int k = 0; k < 7; k++) q[k] += v[k];
+    } else {
+        unsigned long long *q = partials + ((gid >> 6) % rows) * 8;
+        for (int k = 0; k < 7; k++)
+            if (v[k]) atomicAdd(q + k, v[k]);
+    }
+}
+)";
+
 static const char *const kStreamKernel = R"(
 __device__ __forceinline__ void mk_load4(const SParams &p, uint64_t base, int32_t &a, int32_t &b, int32_t &c, int32_t &d)
 {
@@ -1734,7 +1777,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
     const uint32_t tid = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
     const uint64_t tile = 1024u, ntiles = (p.n + tile - 1) / tile;
-    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    MkCount cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
     int32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
     uint64_t t = blockIdx.x;
@@ -1757,10 +1800,6 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base),
                      (t0 & 0xffu) | (t1 & 0xffu) << 8 | (t2 & 0xffu) << 16 | t3 << 24);
             if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base) = make_uint4(s0, s1, s2, s3);
-            count_lane(cnt, s0, t0);
-            count_lane(cnt, s1, t1);
-            count_lane(cnt, s2, t2);
-            count_lane(cnt, s3, t3);
         } else {
             const int32_t ov[4] = {o0, o1, o2, o3};
             const uint32_t sv[4] = {s0, s1, s2, s3}, tv[4] = {t0, t1, t2, t3};
@@ -1769,11 +1808,16 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
                 p.out[base + k] = ov[k];
                 p.status[base + k] = (uint8_t)tv[k];
                 if (p.steps) p.steps[base + k] = sv[k];
-                count_lane(cnt, sv[k], tv[k]);
             }
         }
+        if (p.partials) {
+            mk_count(cnt, base < p.n, s0, t0);
+            mk_count(cnt, base + 1 < p.n, s1, t1);
+            mk_count(cnt, base + 2 < p.n, s2, t2);
+            mk_count(cnt, base + 3 < p.n, s3, t3);
+        }
     }
-    if (p.partials) write_partials(p.partials, gid, cnt);
+    if (p.partials) mk_count_store(p.partials, 0u, gid, cnt);
 }
 
 )";
@@ -1793,9 +1837,8 @@ static const char *const kStreamKernelHeavy = R"(
 extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
 {
     const uint64_t gid = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-    unsigned long long cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t s = 0u, t = 0u;
     if (gid < p.n) {
-        uint32_t s, t;
 #if MK_SLOTS_WAVE_BLOCKED
         // the wave's 64 lanes of slot k are 256 contiguous bytes and its slots
         // follow one another: a wave's stacks are one block (tis_jit.h)
@@ -1813,9 +1856,12 @@ extern "C" __global__ void __launch_bounds__(64) mk_jit_exec(SParams p)
         p.out[gid] = (t & MK_ST_HAS_OUTPUT) ? o : 0;
         p.status[gid] = (uint8_t)t;
         if (p.steps) p.steps[gid] = s;
-        count_lane(cnt, s, t);
     }
-    if (p.partials) add_partials(p.partials, p.part_rows, gid, cnt);
+    if (p.partials) {
+        MkCount cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        mk_count(cnt, gid < p.n, s, t);
+        mk_count_store(p.partials, p.part_rows ? p.part_rows : 1u, gid, cnt);
+    }
 }
 )";
 
@@ -2674,7 +2720,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
 // dispatcher of kMachineKernel) until the call yields.  A call whose budget
 // slice would end inside a superblock hands off (MK_SS_HANDOFF): the lane
 // stops at that superblock's entry, records it, and the interpreter
-// (mk_exec.hip tis_session_import + tis_session) finishes that call and the
+// (mk_exec.hip tis_session, which imports it first) finishes that call and the
 // rest of the burst.  Sessions the interpreter holds (MK_SS_T1) are skipped.
 const char *const kSessionKernel = R"(
 struct SessK {
@@ -2750,6 +2796,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
                                                  : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
     else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;
+    if (shape != JIT_MACHINE) e.s += kStreamCount;
     e.s += shape == JIT_MACHINE ? mk : heavy ? kStreamKernelHeavy : kStreamKernel;
     return e.s;
 }

@@ -7,10 +7,9 @@ Per launch kind (percall: one call per instance per launch; burst: `calls`
 sequential calls per instance in one launch), from the probe's JSON line, the
 rocprofv3 kernel statistics and the PMC passes:
 
-  * launches per call: which kernels ran per launch (mk_sess_exec, the
-    hand-off import kernel tis_session_import, the interpreter tis_session;
-    the last two exit at once when no call was handed off) and their average
-    durations;
+  * launches per call: which kernels ran per launch (mk_sess_exec and the
+    interpreter tis_session, which first imports any call handed off to it
+    and otherwise exits at once) and their average durations;
   * algorithmic bytes of mk_sess_exec per launch, per instance:
       state  2 x (4 B superblock + 8 B x live registers)  (loaded once, stored once)
       calls  k x (8 B int64 input + 4 B out + 1 B status + 4 B steps)
