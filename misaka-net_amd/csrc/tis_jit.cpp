@@ -1322,7 +1322,34 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             // (twice the issue cycles per wave): the first iteration, whose x
             // may be any value, uses med3 (MK_JIT_FLAG_MIN=0: med3 throughout).
             const bool fmin = step == -1 && !std::strcmp(flag, "MK_FLAG_GT") && g.lim->flag_min;
-            if (fmin && g.lim->sat_dec) {
+            const bool gt = !std::strcmp(flag, "MK_FLAG_GT"), lt = !std::strcmp(flag, "MK_FLAG_LT");
+            if (!fmin && g.lim->sat_count && g.lim->sat_dec == 1 && ((gt && step <= -2) || (lt && step >= 1))) {
+                // Counter form (MK_JIT_SAT_COUNT, round 4): a countdown by k
+                // (x > 0, x -= k; or x < 0, x += k) from x1 after the first
+                // iteration runs z = ceil(|x1| / k) more iterations, so each
+                // iteration is one saturating decrement of z (v_sub_u32
+                // clamp: full rate on gfx950) instead of the bump and the
+                // flag (v_mad_i32_i24 + v_med3_i32: half rate each,
+                // tools/probe/valu_rates.hip); x follows from the iterations
+                // run, exactly, at the loop's end -- also when the budget
+                // bound T32 stops it first.
+                const uint64_t k = (uint64_t)(step < 0 ? -step : step);
+                e.line("    it = 1u;");
+                e.line("    x = (int32_t)((uint32_t)x + %uu);", (uint32_t)(int32_t)step);
+                e.line("    (void)f;");
+                e.line("    const int32_t f0 = %s(x);", flag);
+                e.line("    const uint32_t z0 = f0 ? ((uint32_t)(%sx) + %lluu) / %lluu : 0u;", gt ? "" : "-",
+                       (unsigned long long)(k - 1), (unsigned long long)k);
+                e.line("    int32_t z = (int32_t)z0;");
+                e.line("    more = MK_KEEP(z != 0, need);");
+                e.line("    while (more && T32 - it >= %uu) {", uf);
+                e.line("    it += %uu;", uf);
+                for (int u = 0; u < uf; ++u) e.line("    z = MK_SATDEC(z);");
+                e.line("    more = MK_KEEP(z != 0, need);");
+                e.line("    }");
+                e.line("    a = z != 0;");
+                e.line("    x = (int32_t)((uint32_t)x + %uu * (z0 - (uint32_t)z));", (uint32_t)(int32_t)step);
+            } else if (fmin && g.lim->sat_dec) {
                 // Past the first iteration a lane still in the loop has x > 0:
                 // one saturating decrement per iteration (v_sub_u32 clamp), a
                 // lane that left holds 0 and its flag is x != 0.  Lanes that
@@ -2290,6 +2317,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_SAT_DEC", l.sat_dec);
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TS_WAVE", l.ts_wave);
+    flag("MK_JIT_SAT_COUNT", l.sat_count);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
     flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
@@ -2310,7 +2338,10 @@ std::string JitLimits::key() const
              (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)sat_dec, (int)ts_dyn,
              (int)tune_regs,
              lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad);
-    return ts_wave ? std::string(b) + ",tswave=1" : std::string(b);
+    std::string k = b;
+    if (ts_wave) k += ",tswave=1";
+    if (!sat_count) k += ",scount=0";
+    return k;
 }
 
 // Kernel of the machine shape with lane compaction.  One wave per block,

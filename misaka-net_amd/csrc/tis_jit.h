@@ -137,6 +137,10 @@ struct JitLimits {
     // flag being x != 0 (MK_JIT_SAT_DEC=0: sub + min_u32 per iteration;
     // 1: inline asm; 2: LLVM's usub.sat by an opaque 1, no hazard s_nop).
     uint32_t sat_dec = 1;
+    // ... and a countdown by any other step k (x > 0, x -= k; x < 0, x += k)
+    // as one saturating decrement of its remaining-iteration count per
+    // iteration (MK_JIT_SAT_COUNT=0: the bump and a med3 / shift flag).
+    bool sat_count = true;
     // Heavy stream networks whose LDS slots allow fewer than four waves per
     // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
     // mk_exec.hip tune_soft_regs).

@@ -164,7 +164,7 @@ def corpus():
 
 if __name__ == "__main__":
     vecs = [[p, load_program(p)] for p in corpus()]
-    out = os.path.join(HERE, "tokenizer_reference_regex.json")
+    out = os.path.join(HERE, "front", "tokenizer_reference_regex.json")
     with open(out, "w") as f:
         json.dump({"source": "tests/golden/make_tokenizer_golden.py over internal/tis/tokenizer.go's patterns",
                    "vectors": vecs}, f, separators=(",", ":"))

@@ -141,11 +141,16 @@ def test_loop_phases(tmp_path):
 
 
 # The countdown's saturating-decrement forms (MK_JIT_SAT_DEC: 0 sub + min_u32,
-# 2 usub.sat by an opaque 1; the default 1 runs in every other test): every
-# loop path, and C5 over all trip counts and at budgets inside its loops.
-@pytest.mark.parametrize("mode", ["0", "2"])
+# 2 usub.sat by an opaque 1; the default 1 runs in every other test) and the
+# counter form of countdowns by other steps (MK_JIT_SAT_COUNT, default on;
+# "count0" turns it off): every loop path, and C5 over all trip counts and at
+# budgets inside its loops.
+@pytest.mark.parametrize("mode", ["0", "2", "count0", "default"])
 def test_countdown_forms(tmp_path, monkeypatch, mode):
-    monkeypatch.setenv("MK_JIT_SAT_DEC", mode)
+    if mode == "count0":
+        monkeypatch.setenv("MK_JIT_SAT_COUNT", "0")
+    elif mode != "default":
+        monkeypatch.setenv("MK_JIT_SAT_DEC", mode)
     cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
     cases.append(("c5_all_trips", mk.networks.countdown_network(), np.arange(-3, 1024, dtype=np.int64), {}))
     for b in (1, 2, 3, 37, 400, 1500):

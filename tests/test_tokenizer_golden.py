@@ -9,7 +9,7 @@ import os
 import misaka_net_amd as mk
 from oracle import pyoracle as po
 
-VECS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tokenizer_reference_regex.json")))["vectors"]
+VECS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "front", "tokenizer_reference_regex.json")))["vectors"]
 
 
 def _run(fn, err, program):
