@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -252,7 +253,28 @@ def sessions_leg(net, n, calls, stream):
     same = all(torch.equal(u, v) for u, v in zip(a, b))
     plan = sess.plan()
     sess.close()
-    return {"instances": n, "calls_per_instance": calls, **burst, "per_call": per_call,
+    # Byte model of the native sessions kernel (mk_sess_exec; VERDICT r03
+    # item 6): per instance and launch, the state loaded once and stored once
+    # (superblock 4 B + 8 B per live register, mk_session_plan's state_regs),
+    # per call the int64 input, int32 out, u8 status and u32 steps
+    # (program.go:80-92: state kept across calls; master.go:216-219).  The
+    # time is the whole launch's (host clock, both kernels), so `frac` is a
+    # lower bound on mk_sess_exec's own (tools/sess_roofline.py has the
+    # rocprofv3 split, profiles/r04o_sessions_roofline.json).
+    m = re.search(r"state_regs=(\d+)", plan)
+    roof = None
+    if m:
+        state_b, call_b = 2 * (4 + 8 * int(m.group(1))), 8 + 4 + 1 + 4
+        roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK / 1e9,
+                "bytes_per_instance": {"state": state_b, "per_call": call_b},
+                "model": "n x (state + calls x per_call) bytes per launch / launch time (host clock, "
+                         "mk_sess_exec + tis_session)"}
+        for key, res, k in (("burst", burst, calls), ("per_call", per_call, 1)):
+            t = res["ms_per_call"] * 1e-3 * k  # one launch
+            b = n * (state_b + k * call_b)
+            roof[key] = {"bytes_per_launch": b, "achieved": b / t / 1e9, "frac": b / t / HBM_PEAK}
+        roof["frac"] = roof["burst"]["frac"]
+    return {"instances": n, "calls_per_instance": calls, **burst, "per_call": per_call, "roofline": roof,
             "burst_equals_per_call": same, "plan": plan,
             "note": "stateful sessions, inputs resident in HBM: the burst (mk_session_compute_seq_device, "
                     f"{calls} sequential calls per instance in one launch) is the headline; per_call = one "
@@ -549,8 +571,15 @@ def main():
     # I/O is known to cross HBM: the slot bytes are priced at the L2 peak, a
     # lower bound on the memory time, so `frac` stays a bound (<= 1).
     fabric = min(traffic, bytes_per_launch) if traffic else io_bytes
-    t_mem = fabric / HBM_PEAK + (lds_slot_seconds(bytes_per_launch - fabric) if lds_split
-                                 else (bytes_per_launch - fabric) / L2_PEAK)
+    # Split slots (LDS + HBM + registers): the LDS share is what the LDS
+    # instructions moved (PMC SQ_INSTS_LDS x 64 lanes x 4 B, b32-priced);
+    # entries kept in registers cost no memory time.  Without a matching
+    # profile only the I/O is known to move: a lower bound.
+    lds_insts = prof.get("lds", {}).get("SQ_INSTS_LDS") if traffic else None
+    if lds_split:
+        t_mem = fabric / HBM_PEAK + (lds_slot_seconds(lds_insts * 64 * 4) if lds_insts else 0.0)
+    else:
+        t_mem = fabric / HBM_PEAK + (bytes_per_launch - fabric) / L2_PEAK
     hbm = {
         "bound": "hbm",
         "achieved": hbm_achieved / 1e9,
@@ -561,9 +590,11 @@ def main():
         "bytes_per_lane": bytes_per_launch // lanes,
         "bytes_per_launch": bytes_per_launch,
         "launch_us": launch_max * 1e6,
-        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + LDS-resident bytes, half at ds_write_b32's "
-                  "39.3 TB/s and half at ds_read_b32's 78.6 TB/s)"
+        "model": ("peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + LDS bytes of SQ_INSTS_LDS x 256 B, half at "
+                  "ds_write_b32's 39.3 TB/s and half at ds_read_b32's 78.6 TB/s; register-held entries free)"
                   if traffic and lds_split else
+                  "peak = I/O bytes / 8 TB/s: no PMC profile for this launch, so the LDS / HBM / register split of "
+                  "the stack slots is not measured (a lower bound)" if lds_split else
                   "peak = algorithmic bytes / (PMC fabric bytes / 8 TB/s + L2-resident bytes / 34.5 TB/s)"
                   if traffic and bytes_per_launch > fabric * 1.001 else
                   "peak = HBM 8 TB/s; stack slots in LDS (roofline_lds)" if lds_slots else
