@@ -1540,6 +1540,22 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // their unguarded phase from it; the kernel reduces it over the wave for
     // loop variants only, see mk_is_loop).
     Emitter tab; // budget-exit tables of checked variants (before mk_run)
+    // The kernels call mk_run(u, L) under `if (L.sb == u)`; GVN then
+    // replaces u by the lane's L.sb inside the branch and lowers the switch
+    // as a divergent one: a compare-and-mask tree, one level per halving of
+    // the variants.  The kernels pass MK_SCALAR(u), computed before the
+    // branch; as mk_scalar (the module header: an empty asm with an SGPR
+    // result, no instruction, that GVN cannot see through) the switch is a
+    // scalar compare tree, but LLVM then copies the lane registers into and
+    // out of every case.  Measured (r04u, bench launch times, scalar vs
+    // divergent): C5 (36 variants) 123.7 vs 142.7 us, two_stacks (26) 237.8
+    // vs 228.4, dyn_depth (15) 134.6 vs 134.6, jro_heavy (6) 59.0 vs 52.4 ms;
+    // so the scalar switch from 32 reachable variants (MK_JIT_UNIFORM_SW=1|0
+    // forces either).
+    {
+        const bool scalar = g.lim->uniform_sw == 1 || (g.lim->uniform_sw < 0 && g.nreach >= 32);
+        e.line(scalar ? "#define MK_SCALAR(u) mk_scalar(u)" : "#define MK_SCALAR(u) (u)");
+    }
     const size_t fn_start = e.s.size();
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
     e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
@@ -1950,7 +1966,8 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
         // loop variants: the group's largest step count (exec is full here,
         // as the DPP reduction needs; u is uniform)
         const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
-        if (L.sb == u) mk_run(u, L, p.budget, slots, stride, pol, smax);
+        const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
+        if (L.sb == u) mk_run(us, L, p.budget, slots, stride, pol, smax);
     }
     if (p.partials) write_partials(p.partials, gid, cnt);
 }
@@ -1996,15 +2013,25 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
     const uint32_t pol = MK_POLICY;
     (void)wave;
-    // counters, wave-uniform (scalar registers): steps, outputs, lanes, and the four end reasons
+    // counters: steps per lane (one wave sum at the end), the others
+    // wave-uniform (scalar registers): outputs, lanes, and the four end reasons
     uint64_t c_steps = 0u;
     uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
+#if MK_PROF
+    // MK_JIT_PROF: shader-clock cycles per phase, per wave, in place of the
+    // counters (tools/probe/c5_decomp.py reads them from the stats)
+    const uint64_t pf_t0 = MK_T();
+    uint64_t pf_sort = 0u, pf_chunk = 0u, pf_loop = 0u, pf_other = 0u, pf_res = 0u, pf_rounds = 0u, pf_lrounds = 0u;
+#endif
     const uint64_t ntiles = (p.n + MK_TS_T - 1) / MK_TS_T;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * MK_TS_T;
         const uint32_t m = p.n - base < MK_TS_T ? (uint32_t)(p.n - base) : MK_TS_T;
         const bool vec = p.io_vec && m == MK_TS_T;
+#if MK_PROF
+        uint64_t pf_a = MK_T();
+#endif
         // 1. inputs R tid .. R tid + R - 1 of the tile, their range
         int32_t v[MK_TS_R];
         if (vec) {
@@ -2068,6 +2095,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             s_pos[d] = (uint16_t)(MK_TS_R * tid + k);
         }
         __syncthreads();
+#if MK_PROF
+        pf_sort += MK_T() - pf_a;
+        pf_a = MK_T();
+#endif
         // 2. the sorted lanes, 64 per chunk: MK_TS_DYN -- a wave that is
         // free takes the next chunk, highest values first (their loops run
         // longest where trips follow the value), so the waves reach the
@@ -2093,8 +2124,18 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
                 const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
                 if (!actb) break;
                 const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
+#if MK_PROF
+                const uint64_t pf_r = MK_T();
+#endif
                 const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
-                if (L.sb == u) mk_run(u, L, p.budget, slots, p.lanes, pol, smax);
+                const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
+                if (L.sb == u) mk_run(us, L, p.budget, slots, p.lanes, pol, smax);
+#if MK_PROF
+                const uint64_t pf_d = MK_T() - pf_r;
+                if (mk_is_loop(u)) pf_loop += pf_d, ++pf_lrounds;
+                else pf_other += pf_d;
+                ++pf_rounds;
+#endif
             }
             if (live) {
                 const uint32_t at = s_pos[j];
@@ -2103,8 +2144,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
                 s_steps[at] = L.steps;
             }
             const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
-            c_steps += (uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps & 0xffffu) : 0u)) +
-                       ((uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps >> 16) : 0u)) << 16);
+            c_steps += live ? (uint64_t)L.steps : 0u;
             c_out += (uint32_t)__popcll(__ballot(live && (L.st & MK_ST_HAS_OUTPUT)));
             c_done += (uint32_t)__popcll(__ballot(live));
             c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
@@ -2112,6 +2152,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
             c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
         }
+#if MK_PROF
+        pf_chunk += MK_T() - pf_a;
+        pf_a = MK_T();
+#endif
         __syncthreads();
         // 3. results of the tile, in input order
         if (vec) {
@@ -2129,7 +2173,25 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             }
         }
         __syncthreads(); // the next tile reuses the LDS arrays
+#if MK_PROF
+        pf_res += MK_T() - pf_a;
+#endif
     }
+#if MK_PROF
+    if (p.partials && lane == 0u) {
+        unsigned long long *q = p.partials + (gid >> 6) * 8u;
+        q[0] += MK_T() - pf_t0;
+        q[1] += pf_sort;
+        q[2] += pf_chunk;
+        q[3] += pf_loop;
+        q[4] += pf_other;
+        q[5] += pf_res;
+        q[6] += pf_rounds;
+        q[7] += pf_lrounds;
+    }
+    (void)c_steps; (void)c_out; (void)c_done; (void)c_qu; (void)c_bu; (void)c_ov; (void)c_os;
+#else
+    c_steps = wave_sum(c_steps); // whole wave active: the tile loop's bound is uniform
     if (p.partials && lane == 0u) { // this wave's row (write_partials' layout)
         unsigned long long *q = p.partials + (gid >> 6) * 8u;
         q[0] += c_steps;
@@ -2140,6 +2202,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         q[5] += c_ov;
         q[6] += c_os;
     }
+#endif
 }
 )";
 
@@ -2239,7 +2302,8 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
                 if (!actb) break;
                 const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
                 const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
-                if (L.sb == u) mk_run(u, L, p.budget, slots, p.lanes, pol, smax);
+                const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
+                if (L.sb == u) mk_run(us, L, p.budget, slots, p.lanes, pol, smax);
             }
             if (live) {
                 p.out[base + at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
@@ -2323,6 +2387,8 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
     flag("MK_JIT_NARROW", l.narrow);
     flag("MK_JIT_LDS_QUAD", l.lds_quad);
+    if (const char *v = std::getenv("MK_JIT_UNIFORM_SW"); v && *v) l.uniform_sw = v[0] == '1' ? 1 : v[0] == '0' ? 0 : -1;
+    flag("MK_JIT_PROF", l.prof);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2341,6 +2407,8 @@ std::string JitLimits::key() const
     std::string k = b;
     if (ts_wave) k += ",tswave=1";
     if (!sat_count) k += ",scount=0";
+    if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
+    if (prof) k += ",prof=1";
     return k;
 }
 
@@ -2669,8 +2737,15 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
+    if (lim.prof) { // kMachineSortKernel: cycles per phase in place of the counters (MK_JIT_PROF)
+        e.line("#define MK_PROF 1");
+        e.line("#define MK_T() __builtin_amdgcn_s_memtime()");
+    }
     if (lim.ts_wave) e.line("#define MK_WS_R 12u"); // kMachineWaveSortKernel: a wave's tile, inputs per lane
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
+    // the machine lane's dispatch value as an SGPR value GVN cannot equate
+    // with the lane's superblock id (MK_SCALAR, chosen by emit_machine_lane)
+    e.line("MK_FN uint32_t mk_scalar(uint32_t u) { uint32_t r; __asm__(\"\" : \"=s\"(r) : \"0\"(u)); return r; }");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks
     e.line("MK_FN int32_t mk_flag_gt(int32_t x) { int32_t f; __asm__(\"v_med3_i32 %%0, %%1, 0, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");
@@ -2793,7 +2868,8 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
             if (!actb) break;
             const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
             const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
-            if (L.sb == u) mk_run(u, L, p.budget, slots, p.n, MK_POLICY, smax);
+            const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
+            if (L.sb == u) mk_run(us, L, p.budget, slots, p.n, MK_POLICY, smax);
         }
         if (!live || sbv == MK_SS_T1 || sbv == MK_SS_HAND) continue; // the interpreter answers these
         if (run && L.st == MK_SS_HANDOFF) {

@@ -159,6 +159,17 @@ struct JitLimits {
     // b32 accesses).  Off (default): slot s at s * 64 + l.  Measured r03f:
     // C4 D=64 47.6 us with quads vs 24.2 without, D=256 159.5 vs 161.8.
     bool lds_quad = false;
+    // Machine lanes switch on a wave-uniform scalar (MK_SCALAR: the
+    // dispatched variant through an empty SGPR asm) or on the plain value,
+    // which LLVM's GVN swaps for the lane's own superblock id and lowers as
+    // a divergent compare tree (round 4; emit_machine_lane).  -1: scalar
+    // from 32 reachable variants; MK_JIT_UNIFORM_SW=1|0 forces either.
+    int uniform_sw = -1;
+    // Diagnostics: the tile-sorted machine kernel reports shader-clock cycles
+    // per phase (sort, chunks, loop and other variants, results) and its
+    // dispatch rounds in place of the launch's counters (MK_JIT_PROF=1;
+    // tools/probe/c5_decomp.py).  The launch's statistics are then not counts.
+    bool prof = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
