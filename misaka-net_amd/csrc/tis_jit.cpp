@@ -26,6 +26,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -469,6 +471,173 @@ struct OpWriter {
     }
 };
 
+// Closed form of a pop run's register chain (round 4, MK_JIT_LIN_SUM=1, off
+// by default: measured neutral, see JitLimits::lin_sum).  When
+// every op of the period is linear -- LD, LI, MOV, ADD, SUB, ADDI, RSUBI --
+// the registers after j periods are an affine function of their values
+// before them and of the j periods' popped values: r' = sum c_s r_s +
+// sum d_i x_i + c.  C4's pop loop is `sum = 3 * sum + v`, one dependent
+// v_mad_u64_u32 (10.7 cycles at one wave per SIMD) per pop.  (The same
+// network with `sum = sum + v` ran 21.5 against 163.9 us at D = 256,
+// profiles/r04v_chain*.txt -- but there LLVM forwarded the LDS pushes to the
+// pops and summed the pushed sequence itself, so that was no measure of the
+// chain.)  A prefetched block of U periods runs its
+// first U - 1 in closed form -- the popped values combined by a balanced
+// tree (depth log2 of the pops; for C4's geometric weights 3^k each node is
+// one multiply-add, as many as the chain had), one multiply-add per carried
+// register -- and its last period as written.  Integer arithmetic is a ring
+// (mod 2^32 when every register the period writes is narrow, which also
+// makes the sext32 of a hop the identity; else mod 2^64 without truncating
+// operands), so the registers are bit-identical to running the chain.
+struct LinForm {
+    std::vector<uint64_t> reg, ld; // coefficients of the registers before the block, of its popped values
+    uint64_t c = 0;
+};
+
+struct LinSummary {
+    bool ok = false, mod32 = false;
+    std::vector<uint32_t> carried; // registers read before written in the period and written in it
+    std::vector<LinForm> F;        // their values after U - 1 periods
+};
+
+LinSummary lin_summary(const Graph &g, const Run &r, size_t nlds, size_t U)
+{
+    LinSummary S;
+    const size_t NR = g.used_reg.size(), NL = (U - 1) * nlds;
+    std::vector<char> wr(NR, 0), rd(NR, 0), narrow_ok(NR, 0);
+    bool trunc = false;
+    auto read = [&](uint32_t off) {
+        if (!wr[off / 8]) rd[off / 8] = 1;
+    };
+    for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
+        const DOp &I = g.D[pc];
+        switch (I.op) {
+        case U_LD: case U_LI: break;
+        case U_MOV: case U_ADDI: case U_RSUBI: read(I.a); trunc = trunc || (I.fl & UF_TA); break;
+        case U_ADD: case U_SUB:
+            read(I.a), read(I.b);
+            trunc = trunc || (I.fl & (UF_TA | UF_TB));
+            break;
+        default: return S;
+        }
+        if (I.d / 8 >= NR) return S;
+        wr[I.d / 8] = 1;
+    }
+    bool all_narrow = true, any_narrow = false;
+    for (size_t k = 0; k < NR; ++k) {
+        if (!wr[k]) continue;
+        const bool n = k < g.narrow.size() && g.narrow[k];
+        all_narrow = all_narrow && n;
+        any_narrow = any_narrow || n;
+    }
+    if (all_narrow) S.mod32 = true;
+    else if (trunc || any_narrow) return S;
+    const uint64_t M = S.mod32 ? 0xffffffffull : ~0ull;
+    std::vector<LinForm> st(NR);
+    std::vector<char> has(NR, 0);
+    auto zero = [&] {
+        LinForm x;
+        x.reg.assign(NR, 0);
+        x.ld.assign(NL, 0);
+        return x;
+    };
+    auto get = [&](uint32_t off) {
+        const uint32_t k = off / 8;
+        if (has[k]) return st[k];
+        LinForm x = zero();
+        x.reg[k] = 1;
+        return x;
+    };
+    auto comb = [&](const LinForm &a, const LinForm &b, uint64_t sb) { // a + sb * b
+        LinForm x = a;
+        for (size_t k = 0; k < NR; ++k) x.reg[k] = (x.reg[k] + sb * b.reg[k]) & M;
+        for (size_t k = 0; k < NL; ++k) x.ld[k] = (x.ld[k] + sb * b.ld[k]) & M;
+        x.c = (x.c + sb * b.c) & M;
+        return x;
+    };
+    for (size_t it = 0; it + 1 < U; ++it) {
+        size_t a = 0;
+        for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
+            const DOp &I = g.D[pc];
+            LinForm x;
+            switch (I.op) {
+            case U_LD: x = zero(); x.ld[it * nlds + a++] = 1; break;
+            case U_LI: x = zero(); x.c = (uint64_t)I.imm & M; break;
+            case U_MOV: x = get(I.a); break;
+            case U_ADDI: x = get(I.a); x.c = (x.c + (uint64_t)I.imm) & M; break;
+            case U_RSUBI: x = comb(zero(), get(I.a), ~0ull); x.c = (x.c + (uint64_t)I.imm) & M; break;
+            case U_ADD: x = comb(get(I.a), get(I.b), 1); break;
+            case U_SUB: x = comb(get(I.a), get(I.b), ~0ull); break;
+            default: return S;
+            }
+            st[I.d / 8] = x;
+            has[I.d / 8] = 1;
+        }
+    }
+    bool chain = false;
+    for (uint32_t k = 0; k < NR; ++k) {
+        if (!(rd[k] && wr[k])) continue;
+        S.carried.push_back(k);
+        S.F.push_back(has[k] ? st[k] : get(k * 8));
+    }
+    for (const LinForm &f : S.F)
+        for (uint32_t k : S.carried) chain = chain || f.reg[k] != 0;
+    S.ok = chain; // nothing to gain without a register carried through the loop
+    return S;
+}
+
+// Source of sum d_i x_i over the block's popped values (x(i) names value i):
+// a balanced tree of multiply-adds when the weights are geometric with the
+// last nonzero weight 1 (sum a^(e-i) x_i), else a balanced sum of products.
+// Each inner node becomes a named temporary (prefix `tp`), so the tree is the
+// dependence structure LLVM sees.
+template <class Name>
+std::string lin_tree(Emitter &e, const std::vector<uint64_t> &d, bool mod32, const Name &x, const std::string &tp)
+{
+    const char *T = mod32 ? "uint32_t" : "uint64_t";
+    const uint64_t M = mod32 ? 0xffffffffull : ~0ull;
+    long lo = -1, hi = -1;
+    for (size_t i = 0; i < d.size(); ++i)
+        if (d[i]) {
+            if (lo < 0) lo = (long)i;
+            hi = (long)i;
+        }
+    if (lo < 0) return "";
+    int tmp = 0;
+    auto lit = [&](uint64_t v) {
+        char b[40];
+        snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull", T, v & M);
+        return std::string(b);
+    };
+    bool geo = d[hi] == 1;
+    const uint64_t a = hi > lo ? d[hi - 1] : 1;
+    for (long i = lo; geo && i < hi; ++i) geo = d[i] != 0 && d[i] == ((a * d[i + 1]) & M);
+    std::function<std::string(long, long)> node;
+    std::vector<uint64_t> pw(hi - lo + 2, 1); // a^k
+    if (geo) {
+        for (size_t k = 1; k < pw.size(); ++k) pw[k] = (pw[k - 1] * a) & M;
+        node = [&](long l, long h) -> std::string {
+            if (l == h) return x(l);
+            const long m = (l + h + 1) / 2;
+            const std::string L = node(l, m - 1), R = node(m, h);
+            const std::string t = tp + std::to_string(tmp++);
+            e.s += "    const " + std::string(T) + " " + t + " = " + (pw[h - m + 1] == 1 ? L : lit(pw[h - m + 1]) + " * " + L) +
+                   " + " + R + ";\n";
+            return t;
+        };
+    } else {
+        node = [&](long l, long h) -> std::string {
+            if (l == h) return d[l] == 0 ? lit(0) : d[l] == 1 ? x(l) : lit(d[l]) + " * " + x(l);
+            const long m = (l + h + 1) / 2;
+            const std::string L = node(l, m - 1), R = node(m, h);
+            const std::string t = tp + std::to_string(tmp++);
+            e.s += "    const " + std::string(T) + " " + t + " = " + L + " + " + R + ";\n";
+            return t;
+        };
+    }
+    return node(lo, hi);
+}
+
 // A rolled loop whose body only reads stack slots (a run of POPs: LD ops, no
 // ST) is software-pipelined: while one block of U iterations uses its
 // popped values, the slots of the next block are already being read, so a
@@ -510,8 +679,44 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
         // keeps the read-ahead here: LLVM otherwise sinks each load to its use
         e.line("    __asm__ volatile(\"\" ::: \"memory\");");
     };
+    const LinSummary lin = g.lim->lin_sum && U >= 4 ? lin_summary(g, r, lds.size(), U) : LinSummary{};
+    int lin_id = 0;
     auto body = [&](char set, const std::string &it) {
-        for (size_t k = 0; k < U; ++k) {
+        size_t k0 = 0;
+        if (lin.ok) { // periods 0 .. U-2 of the block in closed form (lin_summary)
+            const char *T = lin.mod32 ? "uint32_t" : "uint64_t";
+            const uint64_t M = lin.mod32 ? 0xffffffffull : ~0ull;
+            const std::string id = std::to_string(D) + "_" + std::to_string(lin_id++);
+            e.line("    {");
+            auto xname = [&](long i) {
+                char b[64];
+                snprintf(b, sizeof b, lin.mod32 ? "(uint32_t)%c%zu_%zu_%zu" : "(uint64_t)(int64_t)%c%zu_%zu_%zu", set, D,
+                         (size_t)i % lds.size(), (size_t)i / lds.size());
+                return std::string(b);
+            };
+            for (size_t q = 0; q < lin.carried.size(); ++q) {
+                const LinForm &f = lin.F[q];
+                std::string x = lin_tree(e, f.ld, lin.mod32, xname, "lt" + id + "_" + std::to_string(q) + "_");
+                for (size_t k = 0; k < f.reg.size(); ++k) {
+                    if (!f.reg[k]) continue;
+                    char b[96];
+                    if (f.reg[k] == 1) snprintf(b, sizeof b, "(%s)%s%zu", T, w.R, k);
+                    else snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull * (%s)%s%zu", T, f.reg[k] & M, T, w.R, k);
+                    x = x.empty() ? std::string(b) : std::string(b) + " + " + x;
+                }
+                if (f.c || x.empty()) {
+                    char b[48];
+                    snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull", T, f.c & M);
+                    x = x.empty() ? std::string(b) : x + " + " + b;
+                }
+                e.s += "    const " + std::string(T) + " ln" + id + "_" + std::to_string(q) + " = " + x + ";\n";
+            }
+            for (size_t q = 0; q < lin.carried.size(); ++q)
+                e.line("    %s%u = (%s)ln%s_%zu;", w.R, lin.carried[q], lin.mod32 ? "uint32_t" : "int64_t", id.c_str(), q);
+            e.line("    }");
+            k0 = U - 1;
+        }
+        for (size_t k = k0; k < U; ++k) {
             e.line("    { const uint32_t j%zu = %s + %zuu; (void)j%zu;", D, it.c_str(), k, D);
             for (size_t pc = r.start, a = 0; pc < r.start + r.period; ++pc) {
                 const DOp &I = g.D[pc];
@@ -2389,6 +2594,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_LDS_QUAD", l.lds_quad);
     if (const char *v = std::getenv("MK_JIT_UNIFORM_SW"); v && *v) l.uniform_sw = v[0] == '1' ? 1 : v[0] == '0' ? 0 : -1;
     flag("MK_JIT_PROF", l.prof);
+    flag("MK_JIT_LIN_SUM", l.lin_sum);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2409,6 +2615,7 @@ std::string JitLimits::key() const
     if (!sat_count) k += ",scount=0";
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
+    if (lin_sum) k += ",lsum=1";
     return k;
 }
 

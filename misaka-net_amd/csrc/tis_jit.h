@@ -170,6 +170,14 @@ struct JitLimits {
     // dispatch rounds in place of the launch's counters (MK_JIT_PROF=1;
     // tools/probe/c5_decomp.py).  The launch's statistics are then not counts.
     bool prof = false;
+    // Pop runs whose register updates are linear run each prefetched block's
+    // first periods in closed form, the popped values combined by a tree
+    // (tis_jit.cpp lin_summary; MK_JIT_LIN_SUM=1).  Bit-exact, and measured
+    // neutral (r04w: C4 d256 158.1 vs 159.9 us, d1024 2,324 vs 2,320 us): at
+    // one wave per SIMD a wave issues one VALU op per ~8.8 cycles whether or
+    // not it depends on the previous one (tools/probe/valu_rates.hip), so a
+    // shorter chain of the same ops does not shorten the wave.  Off.
+    bool lin_sum = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key

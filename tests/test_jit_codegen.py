@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import misaka_net_amd as mk
+from misaka_net_amd.network import NodeSpec
 from oracle import pyoracle as po
 import schedcheck as sc
 from tisgen import census_classes, stack_loop_network, loop_cases, random_network
@@ -329,3 +330,52 @@ def test_modules_are_code_object_v5(tmp_path, monkeypatch):
     assert plan.startswith("tier=native"), plan
     hdr = subprocess.run([readelf, "-h", co], capture_output=True, text=True, check=True).stdout
     assert any(l.split() == ["ABI", "Version:", "3"] for l in hdr.splitlines()), hdr
+
+
+def _pop_chain_program(accum: str, depth: int, tail: str = "SWP\nOUT ACC") -> str:
+    """One node: push x + 7k (k = 1..depth), then pop every value into an
+    accumulator kept in BAK through `accum` (ACC holds the running value, R2
+    the popped one), the loop counter in the node's own port R1."""
+    return "\n".join([
+        "IN ACC", "SAV", f"MOV {depth}, ACC",
+        "L: SWP", "ADD 7", "PUSH ACC, s", "SWP", "SUB 1", "JGZ L",
+        "MOV 0, ACC", "SAV", f"MOV {depth}, ACC", "MOV ACC, a:R1",
+        "Q: POP s, ACC", "MOV ACC, a:R2", "SWP", accum, "SAV",
+        "MOV R1, ACC", "SUB 1", "MOV ACC, a:R1", "JGZ Q",
+        "MOV R1, NIL", tail, ""])
+
+
+POP_CHAINS = {
+    "mul3": "MOV ACC, a:R3\nADD ACC\nADD R3\nADD R2",      # C4's sum = 3 * sum + v
+    "add": "ADD R2",                                       # sum + v
+    "sub": "SUB R2",                                       # sum - v
+    "mul2": "ADD ACC\nADD R2",                             # 2 * sum + v
+    "mul4c": "ADD ACC\nADD ACC\nADD R2\nADD 5",            # 4 * sum + v + 5
+    "neg": "NEG\nADD R2",                                  # v - sum
+    "mul5": "MOV ACC, a:R3\nADD ACC\nADD ACC\nADD R3\nSUB R2",  # 5 * sum - v
+}
+
+
+@pytest.mark.parametrize("lin", ["1", "0"])
+@pytest.mark.parametrize("tail", ["out", "sign"])
+def test_pop_chain_closed_form(tmp_path, monkeypatch, lin, tail):
+    """Pop runs in closed form (tis_jit.cpp lin_summary, MK_JIT_LIN_SUM): every
+    linear accumulation, read only through hops (narrow: mod 2^32) or by a
+    sign test (wide: mod 2^64, no truncating operand), bit-exact against the
+    oracle on full-range inputs (INT32_MIN/MAX included), with the closed
+    form present in the source where it applies."""
+    monkeypatch.setenv("MK_JIT_LIN_SUM", lin)
+    t = "SWP\nOUT ACC" if tail == "out" else "SWP\nJGZ P\nOUT 1\nJMP E\nP: OUT ACC\nE: NOP"
+    cases, srcs = [], {}
+    for name, accum in POP_CHAINS.items():
+        nodes = [NodeSpec("a", "program", _pop_chain_program(accum, 100, t)), NodeSpec("s", "stack", "")]
+        cases.append((f"{name}-{tail}", nodes, po.gen_inputs(SEED, 300), {}))
+        srcs[name] = sc.jit_lane(nodes)[0]
+    check_cases(tmp_path, cases)
+    closed = {n for n, s in srcs.items() if "const uint32_t ln" in s or "const uint64_t ln" in s}
+    if lin == "0":
+        assert not closed
+    elif tail == "out":  # narrow accumulators: every chain in closed form
+        assert closed == set(POP_CHAINS), closed
+    else:
+        assert closed, "no wide chain in closed form"
