@@ -71,6 +71,9 @@ extern char **environ;
 namespace mk {
 
 constexpr int kBlock = 256;
+// The session interpreter's grid cap (blocks of kBlock, grid-stride beyond):
+// 8 blocks per CU of the 256, more than its register state lets reside.
+constexpr uint64_t kSessGridCap = 2048;
 // Native sessions' markers (tis_jit.cpp MK_SS_*; 0xFFFFFFF0 = ended): held by
 // the interpreter, handed off in this launch.
 constexpr uint32_t kSessDead = 0xFFFFFFF0u, kSessT1 = 0xFFFFFFF1u, kSessHand = 0xFFFFFFF2u;
@@ -1039,23 +1042,18 @@ __device__ __forceinline__ void sess_import_one(const SessImport &q, const SessP
     atomicAdd(&q.sflags[1], 1u);
 }
 
+// One session instance (gid) of the interpreter kernel below; `handed`: the
+// native tier handed calls off in this launch, to be imported first.
 template <int NMAX>
-__global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ code, SessParams p)
+__device__ __forceinline__ void tis_session_one(const Insn *__restrict__ code, const SessParams &p, const uint64_t gid,
+                                                int32_t *const lds, const bool handed)
 {
-    extern __shared__ int32_t lds[];
     const int B = kBlock;
     const int tid = threadIdx.x;
-    const uint64_t gid = (uint64_t)blockIdx.x * B + tid;
     const uint64_t n = p.n;
     int32_t *const port = lds;                     // [nprog*4][B]
     int32_t *const sdepth = lds + p.nprog * 4 * B; // [nstack][B]
-    if (p.fuse_import) {
-        const bool handed = p.imp.sflags[0] == p.imp.epoch; // something was handed off in this launch
-        if (!handed && !p.resume && p.sflags[1] == 0u) return; // every session is the native tier's
-        if (handed) sess_import_one(p.imp, p, gid);
-    } else if (p.nsb && !p.resume && p.sflags[1] == 0u) {
-        return; // every session is the native tier's
-    }
+    if (handed) sess_import_one(p.imp, p, gid);
     const bool live = gid < n && (!p.nsb || p.nsb[gid] == kSessT1);
 
     int64_t acc[NMAX], bak[NMAX];
@@ -1347,6 +1345,28 @@ __global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ c
     p.io[gid] = (in_full ? 1u : 0u) | (out_full ? 2u : 0u) | (io & 0xCu) | (dead << 4);
     p.in_val[gid] = in_val;
     p.out_val[gid] = out_val;
+}
+
+// The interpreter over the session set, grid-stride: the grid is capped
+// (kSessGridCap blocks), so a launch in which every session is the native
+// tier's -- the common case, each thread leaving at the flag test -- costs
+// a small grid instead of one block per 256 sessions (round 4: the per-call
+// launch pair's second half).
+template <int NMAX>
+__global__ void __launch_bounds__(kBlock) tis_session(const Insn *__restrict__ code, SessParams p)
+{
+    extern __shared__ int32_t lds[];
+    bool handed = false;
+    if (p.fuse_import) {
+        handed = p.imp.sflags[0] == p.imp.epoch; // something was handed off in this launch
+        if (!handed && !p.resume && p.sflags[1] == 0u) return; // every session is the native tier's
+    } else if (p.nsb && !p.resume && p.sflags[1] == 0u) {
+        return; // every session is the native tier's
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t end = (p.n + kBlock - 1) / kBlock * kBlock; // whole blocks: every thread takes the same trips
+    for (uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x; gid < end; gid += stride)
+        tis_session_one<NMAX>(code, p, gid, lds, handed);
 }
 
 // mk_session_cancel: abandon every open call (io bits 2-3); the state the
@@ -3028,6 +3048,7 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
     const size_t lds = (size_t)(s->nprog * 4 + s->nstack) * kBlock * 4;
     const uint64_t blocks = (s->n + kBlock - 1) / kBlock;
     if (blocks > 0x7fffffffull) return MK_ELIMIT;
+    const uint64_t iblocks = blocks < kSessGridCap ? blocks : kSessGridCap; // the interpreter's grid-stride grid
     if (s->native && !resume) {
         if (++s->epoch == 0) s->epoch = 1; // sflags[0] starts at 0: "no hand-off yet"
         // 1. the native kernel: every session it holds, every call of the burst
@@ -3045,7 +3066,7 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
-    if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)blocks), dim3(kBlock), args, lds, stream) !=
+    if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)iblocks), dim3(kBlock), args, lds, stream) !=
         hipSuccess) {
         if (s->native && !resume) s->broken = true;
         return MK_EDEVICE;
