@@ -2274,7 +2274,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         const uint32_t sh = bits > 8u ? bits - 8u : 0u;
         uint32_t bk[MK_TS_R];
         for (uint32_t k = 0; k < MK_TS_R; ++k) {
-            bk[k] = (((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh;
+            // a tile of one value (span 0) goes by position, bucket tid: its
+            // 1,024 atomics on one bucket would serialize (C5 with every input
+            // 0 spent half its time here, profiles/r04r_c5_phase_prof.jsonl)
+            bk[k] = span ? (((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh : tid;
             if (MK_TS_R * tid + k < m) atomicAdd(&s_cnt[bk[k]], 1u);
         }
         __syncthreads();
@@ -2951,8 +2954,10 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_wave) e.line("#define MK_WS_R 12u"); // kMachineWaveSortKernel: a wave's tile, inputs per lane
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // the machine lane's dispatch value as an SGPR value GVN cannot equate
-    // with the lane's superblock id (MK_SCALAR, chosen by emit_machine_lane)
-    e.line("MK_FN uint32_t mk_scalar(uint32_t u) { uint32_t r; __asm__(\"\" : \"=s\"(r) : \"0\"(u)); return r; }");
+    // with the lane's superblock id (MK_SCALAR, chosen by emit_machine_lane;
+    // machine modules only, so the stream modules' sources stay as they were)
+    if (shape == JIT_MACHINE)
+        e.line("MK_FN uint32_t mk_scalar(uint32_t u) { uint32_t r; __asm__(\"\" : \"=s\"(r) : \"0\"(u)); return r; }");
     // int 0/1 loop flags and the predicated bump (emit_self_loop, narrow
     // phase); inline asm so that LLVM does not turn them back into lane masks
     e.line("MK_FN int32_t mk_flag_gt(int32_t x) { int32_t f; __asm__(\"v_med3_i32 %%0, %%1, 0, 1\" : \"=v\"(f) : \"v\"(x)); return f; }");

@@ -871,3 +871,30 @@ def test_session_device_bursts_match_oracle(gpu, seed):
                                          sp[c].cpu().numpy().astype(np.uint32))
             assert_same(got, refs[c], f"burst={burst} call {c}")
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill", ["zeros", "sevens", "halves"])
+def test_machine_tiles_of_equal_inputs(gpu, fill):
+    """The tile-sorted machine kernel skips its histogram when a tile holds
+    one value (tis_jit.cpp kMachineSortKernel, span 0): C5 over all-equal
+    tiles, a partial last tile, and tiles mixing one repeated value with
+    ordinary inputs, bit-exact against the oracle with the counters."""
+    import torch
+
+    n = 3 * 1024 + 517  # three whole tiles of 1,024 and a partial one
+    xs = np.zeros(n, np.int64)
+    if fill == "sevens":
+        xs[:] = 7
+    elif fill == "halves":  # every other tile one value, the others random
+        xs[:] = po.gen_inputs(SEED, n, kind=N.MK_GEN_MASKED, mask=1023)
+        for t in range(0, n, 2048):
+            xs[t:t + 1024] = 300
+    nodes = mk.networks.countdown_network()
+    net = mk.Network(nodes)
+    assert "shape=machine" in net.plan()
+    got = _device_run(net, n, in_tensor=torch.from_numpy(xs.astype(np.int32)).cuda(), in_kind=N.MK_IN_I32)
+    ref = po.OracleNet(nodes).compute_batch(xs)
+    for g_, r_ in zip(got[:3], ref[:3]):
+        np.testing.assert_array_equal(g_, r_)
+    assert int(got[3][0]) == int(np.asarray(ref[2], np.uint64).sum())  # retired steps
