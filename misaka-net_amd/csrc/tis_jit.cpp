@@ -1359,7 +1359,8 @@ const char *int_flag_fn(const DOp &X, uint32_t v, int ind, size_t body_ops, int6
     return nullptr;
 }
 
-void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
+void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc,
+                    const std::string &chain = std::string())
 {
     Emitter &e = w.e;
     const DOp &G = g.D[gpc], &X = g.D[xpc];
@@ -1641,8 +1642,20 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         else if (tk != v) cl = "!" + l.cond(X);
     }
     e.line("    L.sb = (a || (%s)) ? (L.steps < lim ? %uu : %uu) : %uu;", cl.c_str(), v, (uint32_t)G.imm, other);
+    e.s += chain;
     e.line("    break;");
     e.line("    }");
+}
+
+// The variant a self-loop leaves to (emit_self_loop's `other`), or ~0u.
+uint32_t loop_exit_target(const Graph &g, uint32_t v, size_t xpc)
+{
+    const DOp &X = g.D[xpc];
+    if (X.op != U_BR) return ~0u;
+    const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
+    if (tk == v && nt != v) return nt;
+    if (tk != v) return tk;
+    return ~0u;
 }
 
 void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
@@ -1761,6 +1774,83 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         const bool scalar = g.lim->uniform_sw == 1 || (g.lim->uniform_sw < 0 && g.nreach >= 32);
         e.line(scalar ? "#define MK_SCALAR(u) mk_scalar(u)" : "#define MK_SCALAR(u) (u)");
     }
+    // Chaining (round 4, MK_JIT_CHAIN=1; off by default: measured slower, see
+    // JitLimits::chain): a variant whose lanes all go on to
+    // the same next variant w continues there directly (`goto MKV<w>`)
+    // instead of returning to the kernel's dispatcher -- no ballot, readlane
+    // and compare tree for that round.  Only to variants that are not loops
+    // (their unguarded phase needs the wave-wide step maximum, which the
+    // dispatcher computes with the whole wave active) and only along forward
+    // edges of a depth-first order from variant 0, so the gotos add no cycle
+    // and the control flow stays reducible.  A lane that left early (a
+    // budget guard, a side exit) has another L.sb and keeps the chain off
+    // for the group; lanes not in the group wait for the dispatcher as
+    // before.  Sessions keep the plain dispatcher, and so do lanes of more
+    // than 64 reachable variants: the gotos multiply the paths LLVM's
+    // structurizer sees (a 282-variant census network took hiprtc 44 s
+    // without them and over 120 s with them).
+    std::vector<char> is_loop(nv, 0), chain_to(nv, 0), targeted(nv, 0);
+    std::vector<uint32_t> rpo(nv, 0);
+    const bool chain = g.lim->chain && !p.session && g.nreach <= 64;
+    if (chain) {
+        auto succs = [&](uint32_t v, std::vector<uint32_t> &out) {
+            out.clear();
+            for (size_t pc = g.entry[v];; ++pc) {
+                const DOp &I = g.D[pc];
+                if (I.op == U_GUARD || I.op == U_BRX) out.push_back((uint32_t)I.imm);
+                else if (I.op == U_JUMP) { out.push_back((uint32_t)I.imm); break; }
+                else if (I.op == U_BR) {
+                    out.push_back((uint32_t)(uint64_t)I.imm);
+                    out.push_back((uint32_t)((uint64_t)I.imm >> 32));
+                    break;
+                } else if (I.op == U_JRO) {
+                    for (uint64_t t = 0; t <= I.b; ++t) out.push_back(p.jtab[(size_t)I.imm + t]);
+                    break;
+                } else if (I.op == U_END || I.op == U_YIELD || I.op == U_HANDOFF) break;
+            }
+        };
+        // postorder by an explicit stack, then reversed
+        std::vector<char> state(nv, 0);
+        std::vector<uint32_t> post, sv;
+        std::vector<std::pair<uint32_t, size_t>> st{{0u, 0}};
+        std::vector<std::vector<uint32_t>> sc(nv);
+        state[0] = 1;
+        succs(0, sc[0]);
+        while (!st.empty()) {
+            auto &[v, i] = st.back();
+            if (i < sc[v].size()) {
+                const uint32_t t = sc[v][i++];
+                if (t < nv && g.seen[t] && !state[t]) {
+                    state[t] = 1;
+                    succs(t, sc[t]);
+                    st.push_back({t, 0});
+                }
+                continue;
+            }
+            post.push_back(v);
+            st.pop_back();
+        }
+        for (size_t k = 0; k < post.size(); ++k) rpo[post[k]] = (uint32_t)(post.size() - 1 - k);
+        for (uint32_t v = 0; v < nv; ++v) {
+            if (!g.seen[v]) continue;
+            size_t gpc = 0, xpc = 0;
+            is_loop[v] = self_loop(g, v, gpc, xpc);
+            size_t lo, hi;
+            body_range(g, v, lo, hi);
+            const RoundEnds re = round_ends(g, v, lo, hi);
+            const bool checked = !re.segs.empty() && !has_inline_exit(g, lo, hi);
+            chain_to[v] = state[v] && !is_loop[v] && !checked;
+        }
+    }
+    auto chain_line = [&](uint32_t from, uint32_t to) -> std::string {
+        if (!chain || to >= nv || to == from || !chain_to[to] || !g.seen[from] || rpo[to] <= rpo[from]) return "";
+        targeted[to] = 1;
+        char b[96];
+        snprintf(b, sizeof b, "    if (MK_ALL(L.sb == %uu)) goto MKV%u;\n", to, to);
+        return b;
+    };
+    std::string run_src; // mk_run's cases, emitted once the chain targets are known (labels)
+    std::swap(run_src, e.s);
     const size_t fn_start = e.s.size();
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
     e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
@@ -1770,10 +1860,11 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     for (uint32_t v = 0; v < nv; ++v) {
         if (!g.seen[v]) continue;
         e.line("    case %uu: {", v);
+        e.line("    MKL%u_", v); // the chain label, if a chain targets v (resolved below)
         size_t gpc = 0, xpc = 0;
         if (self_loop(g, v, gpc, xpc)) {
             loops.push_back(v);
-            emit_self_loop(w, g, v, gpc, xpc);
+            emit_self_loop(w, g, v, gpc, xpc, chain_line(v, loop_exit_target(g, v, xpc)));
             continue;
         }
         // early exits jump to X<v>, the end of the case
@@ -1812,11 +1903,15 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         case U_JUMP:
             e.line("    L.steps += %uu;", I.inc);
             e.line("    L.sb = %uu;", (uint32_t)I.imm);
+            e.s += chain_line(v, (uint32_t)I.imm);
             break;
         case U_BR:
             e.line("    L.steps += %uu;", I.inc);
             e.line("    L.sb = %s ? %uu : %uu;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm,
                    (uint32_t)((uint64_t)I.imm >> 32));
+            e.s += chain_line(v, (uint32_t)(uint64_t)I.imm);
+            if ((uint32_t)((uint64_t)I.imm >> 32) != (uint32_t)(uint64_t)I.imm)
+                e.s += chain_line(v, (uint32_t)((uint64_t)I.imm >> 32));
             break;
         case U_JRO: {
             e.line("    L.steps += %uu;", I.inc);
@@ -1866,6 +1961,15 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    }");
     e.line("}");
     e.s.insert(fn_start, tab.s);
+    // chain labels: `MKV<v>: ;` where a chain targets v, nothing elsewhere
+    for (uint32_t v = 0; v < nv; ++v) {
+        const std::string mark = "    MKL" + std::to_string(v) + "_\n";
+        const size_t at = e.s.find(mark);
+        if (at == std::string::npos) continue;
+        e.s.replace(at, mark.size(), targeted[v] ? "    MKV" + std::to_string(v) + ": ;\n" : std::string());
+    }
+    run_src += e.s;
+    std::swap(run_src, e.s);
     e.line("// %zu self-loops", loops.size());
     e.line("MK_FN bool mk_is_loop(const uint32_t u)");
     e.line("{");
@@ -2598,6 +2702,7 @@ JitLimits JitLimits::from_env()
     if (const char *v = std::getenv("MK_JIT_UNIFORM_SW"); v && *v) l.uniform_sw = v[0] == '1' ? 1 : v[0] == '0' ? 0 : -1;
     flag("MK_JIT_PROF", l.prof);
     flag("MK_JIT_LIN_SUM", l.lin_sum);
+    flag("MK_JIT_CHAIN", l.chain);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2619,6 +2724,7 @@ std::string JitLimits::key() const
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
     if (lin_sum) k += ",lsum=1";
+    if (chain) k += ",chain=1";
     return k;
 }
 

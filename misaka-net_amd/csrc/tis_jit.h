@@ -178,6 +178,13 @@ struct JitLimits {
     // not it depends on the previous one (tools/probe/valu_rates.hip), so a
     // shorter chain of the same ops does not shorten the wave.  Off.
     bool lin_sum = false;
+    // Machine lanes continue straight into the next variant when all of a
+    // group's lanes go there (tis_jit.cpp emit_machine_lane; MK_JIT_CHAIN=1).
+    // Measured slower (r05d, launch times, chained vs dispatcher): C5 139.9 vs
+    // 123.5 us (77 -> 83 VGPRs), two_stacks 242.3 vs 230.1, dyn_depth 136.3
+    // vs 132.9 -- the extra paths cost more than the dispatch rounds saved.
+    // Off.
+    bool chain = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key

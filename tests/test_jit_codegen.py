@@ -379,3 +379,17 @@ def test_pop_chain_closed_form(tmp_path, monkeypatch, lin, tail):
         assert closed == set(POP_CHAINS), closed
     else:
         assert closed, "no wide chain in closed form"
+
+
+def test_chained_variants(tmp_path, monkeypatch):
+    """Opt-in variant chaining (MK_JIT_CHAIN=1, emit_machine_lane): the
+    machine lane's gotos between variants, on the configs and random
+    networks, bit-exact against the oracle; the chains are present."""
+    monkeypatch.setenv("MK_JIT_CHAIN", "1")
+    cases = [("c5", mk.networks.countdown_network(), po.gen_inputs(SEED, 1500, kind=1, mask=1023), {}),
+             ("c5_budget", mk.networks.countdown_network(), po.gen_inputs(SEED, 600, kind=1, mask=1023),
+              {"budget": 777})]
+    for seed in (3, 5, 9, 17, 41):
+        cases.append((f"seed{seed}", random_network(seed), po.gen_inputs(seed, 300), {"budget": [97, 5000][seed % 2]}))
+    check_cases(tmp_path, cases, machine=True)
+    assert "goto MKV" in sc.jit_lane(mk.networks.countdown_network(), machine=True)[0]
