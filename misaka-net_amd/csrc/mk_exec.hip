@@ -55,6 +55,7 @@ extern char **environ;
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -2344,14 +2345,21 @@ void rtc_drain_at_exit();
 
 // This ROCm's hiprtc in a namespace of its own, opened once per process and
 // never closed; null (with the reason) when it cannot be opened.
-const RtcApi *ns_rtc(std::string &why)
+// Namespaces the compiler may open: one per compile worker (NsPool).
+constexpr size_t kNsMax = 4;
+
+// This ROCm's hiprtc in namespace k, opened on first use (by worker k's
+// thread, see NsCompiler).
+const RtcApi *ns_rtc(size_t k, std::string &why)
 {
-    static std::string fail;
-    static const RtcApi *api = []() -> const RtcApi * {
+    static std::string fail[kNsMax];
+    static const RtcApi *api[kNsMax];
+    static std::once_flag once[kNsMax];
+    std::call_once(once[k], [k] { api[k] = [k]() -> const RtcApi * {
         void *h = dlmopen(LM_ID_NEWLM, MK_ROCM_LIB "/libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
         if (!h) {
             const char *d = dlerror();
-            fail = std::string("dlmopen: ") + (d ? d : "failed");
+            fail[k] = std::string("dlmopen: ") + (d ? d : "failed");
             return nullptr;
         }
         auto *a = new RtcApi{};
@@ -2366,7 +2374,7 @@ const RtcApi *ns_rtc(std::string &why)
         a->environ_ns = reinterpret_cast<char ***>(dlsym(h, "__environ"));
         if (!a->create || !a->compile || !a->log_size || !a->log || !a->code_size || !a->code || !a->destroy ||
             !a->error || !a->environ_ns) {
-            fail = "dlmopen: hiprtc symbols missing";
+            fail[k] = "dlmopen: hiprtc symbols missing";
             delete a;
             return nullptr;
         }
@@ -2375,63 +2383,126 @@ const RtcApi *ns_rtc(std::string &why)
         // so this drain (registered after them) runs first.
         (void)std::atexit(rtc_drain_at_exit);
         return a;
-    }();
-    why = fail;
-    return api;
+    }(); });
+    why = fail[k];
+    return api[k];
 }
 
-// Every compile in the namespace runs on this one thread, which also opens
-// it, and which never exits.  The namespace's libc keeps per-thread state
-// (ctype tables, malloc's thread cache, thread_local destructor lists) that
-// only the opening thread gets initialised, and that threads started by the
+// Every compile in a namespace runs on one thread, which also opens it, and
+// which never exits.  The namespace's libc keeps per-thread state (ctype
+// tables, malloc's thread cache, thread_local destructor lists) that only
+// the opening thread gets initialised, and that threads started by the
 // process's own libc leave behind unrun when they end: compiles on
 // short-lived threads crashed now and then in comgr (r04a, CPU reproduction).
 class NsCompiler {
   public:
-    static NsCompiler &get()
-    {
-        static NsCompiler *w = new NsCompiler(); // never destroyed: the thread outlives every caller
-        return *w;
-    }
-    // Runs f on the compile thread and returns when it has.
-    void run(const std::function<void()> &f)
+    explicit NsCompiler(size_t k) : k_(k) { spawn_compile_thread([this] { loop(); }); }
+    size_t index() const { return k_; }
+    // Queues f for the compile thread and returns when it has run.
+    void run(const std::shared_ptr<HiprtcJob> &j, const std::function<void()> &f)
     {
         auto done = std::make_shared<std::pair<std::mutex, std::condition_variable>>();
         bool finished = false;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            q_.push_back([&f, &finished, done] {
-                f();
-                std::lock_guard<std::mutex> g(done->first);
-                finished = true;
-                done->second.notify_all();
-            });
+            q_.push_back({j, [&f, &finished, done] {
+                              f();
+                              std::lock_guard<std::mutex> g(done->first);
+                              finished = true;
+                              done->second.notify_all();
+                          }});
         }
         cv_.notify_one();
         std::unique_lock<std::mutex> lk(done->first);
         done->second.wait(lk, [&] { return finished; });
     }
+    // Busy with a compile its caller has given up on (rtc_compile's bound):
+    // a job queued here would wait for it.
+    bool stuck()
+    {
+        std::shared_ptr<HiprtcJob> cur;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cur = cur_;
+        }
+        if (!cur) return false;
+        std::lock_guard<std::mutex> g(cur->mu);
+        return cur->abandoned;
+    }
 
   private:
-    NsCompiler() { spawn_compile_thread([this] { loop(); }); }
     void loop()
     {
         for (;;) {
-            std::function<void()> job;
+            std::pair<std::shared_ptr<HiprtcJob>, std::function<void()>> job;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [this] { return !q_.empty(); });
                 job = std::move(q_.front());
                 q_.pop_front();
+                cur_ = job.first;
             }
-            job();
+            job.second();
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                cur_.reset();
+            }
             segv_trace_check();
         }
     }
+    size_t k_;
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<std::function<void()>> q_;
+    std::deque<std::pair<std::shared_ptr<HiprtcJob>, std::function<void()>>> q_;
+    std::shared_ptr<HiprtcJob> cur_; // the job running now (under mu_)
 };
+
+// The namespace compile workers.  A compile that outlives its bound keeps
+// its worker (and that copy of LLVM) busy until it ends; the next compile
+// goes to the first worker that is not stuck so, opening another namespace
+// (up to kNsMax) when all are -- before, one pathological module held up
+// every later network's compile until its own bound, each then falling
+// back to tier 2 (r05c: a 282-variant census network).  Workers never exit.
+class NsPool {
+  public:
+    static NsPool &get()
+    {
+        static NsPool *p = new NsPool(); // never destroyed: the threads outlive every caller
+        return *p;
+    }
+    NsCompiler &pick()
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (NsCompiler *w : ws_)
+            if (!w->stuck()) return *w;
+        if (ws_.size() < kNsMax) {
+            ws_.push_back(new NsCompiler(ws_.size()));
+            return *ws_.back();
+        }
+        return *ws_.front(); // all stuck: wait behind the first
+    }
+
+  private:
+    std::mutex mu_;
+    std::vector<NsCompiler *> ws_;
+};
+
+// A linked (in-process, this namespace) compile that outlived its bound:
+// the next compile takes a namespace worker instead of queueing behind it
+// in the same comgr.
+std::mutex g_linked_mu;
+std::vector<std::weak_ptr<HiprtcJob>> g_linked_running;
+
+bool linked_stuck()
+{
+    std::lock_guard<std::mutex> lk(g_linked_mu);
+    for (auto &w : g_linked_running)
+        if (auto j = w.lock()) {
+            std::lock_guard<std::mutex> g(j->mu);
+            if (j->abandoned && !j->done) return true;
+        }
+    return false;
+}
 
 bool write_file(const std::string &path, const std::string &data)
 {
@@ -2520,8 +2591,21 @@ constexpr const char *kCodeObjectVersion = "-mcode-object-version=5";
 // compile thread touches it.
 void ns_environ_refresh(const RtcApi &rt)
 {
-    static std::vector<std::string> strings;
-    static std::vector<char *> ptrs;
+    // one copy per namespace (its worker alone refreshes it): a refresh for
+    // one namespace must not free the strings another's compile still reads
+    struct Env {
+        std::vector<std::string> strings;
+        std::vector<char *> ptrs;
+    };
+    static std::mutex mu;
+    static std::map<char ***, Env> envs;
+    Env *env;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        env = &envs[rt.environ_ns]; // map nodes are stable
+    }
+    std::vector<std::string> &strings = env->strings;
+    std::vector<char *> &ptrs = env->ptrs;
     std::vector<std::string> s;
     for (char **e = environ; e && *e; ++e) s.emplace_back(*e);
     std::vector<char *> p;
@@ -2581,9 +2665,10 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     if (ch.kind == RTC_HELPER && !ch.helper.empty()) {
         ran = rtc_spawn(ch.helper, *j, ok, why, code);
         from = "helper";
-    } else if (ch.kind == RTC_NS) {
-        NsCompiler::get().run([&] {
-            if (const RtcApi *rt = ns_rtc(why)) {
+    } else if (ch.kind == RTC_NS || (ch.kind == RTC_LINKED && linked_stuck())) {
+        NsCompiler &w = NsPool::get().pick();
+        w.run(j, [&] {
+            if (const RtcApi *rt = ns_rtc(w.index(), why)) {
                 rtc_inproc(*rt, j->src, ok, why, code);
                 ran = true;
                 from = "ns";
@@ -2592,6 +2677,13 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     }
     if (!ran && !rtc_abandoned(*j)) {
         why.clear();
+        {
+            std::lock_guard<std::mutex> lk(g_linked_mu);
+            g_linked_running.erase(std::remove_if(g_linked_running.begin(), g_linked_running.end(),
+                                                  [](const std::weak_ptr<HiprtcJob> &w) { return w.expired(); }),
+                                   g_linked_running.end());
+            g_linked_running.push_back(j);
+        }
         rtc_inproc(kLinkedRtc, j->src, ok, why, code);
         from = inproc_rtc_differs() ? "linked-other" : "linked";
     }

@@ -140,3 +140,27 @@ print("RESULT", a, b)
                        env=e)
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
     assert r.stdout.split()[-2:] == ["ns", "ns"], r.stdout
+
+
+@pytest.mark.parametrize("mode", ["linked", "ns"])
+def test_compile_past_its_bound_does_not_hold_the_next(mode):
+    """A compile that outlives its bound (MK_JIT_COMPILE_S) keeps its LLVM
+    busy until it ends; the next network's compile takes another namespace
+    worker (NsPool) instead of waiting out its own bound behind it and falling
+    back to tier 2.  AMD_COMGR_CACHE=0: the slow module really compiles."""
+    code = r"""
+import os, sys, time
+sys.path[:0] = [{root!r}]
+import misaka_net_amd as mk
+big = mk.Network(mk.networks.pipeline_network(256)).plan()
+t = time.time()
+small = mk.Network(mk.networks.example_network()).plan()
+print("RESULT", big.split()[0], small.split()[0], round(time.time() - t, 2), flush=True)
+"""
+    e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_COMPILE_S="2", AMD_COMGR_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True, timeout=600,
+                       env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _, big, small, secs = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1].split()
+    assert big == "tier=compiled", big  # D = 256 takes hiprtc ~10 s: past the 2 s bound
+    assert small == "tier=native" and float(secs) < 2.0, (small, secs)
