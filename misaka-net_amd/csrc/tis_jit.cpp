@@ -1529,7 +1529,8 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             // may be any value, uses med3 (MK_JIT_FLAG_MIN=0: med3 throughout).
             const bool fmin = step == -1 && !std::strcmp(flag, "MK_FLAG_GT") && g.lim->flag_min;
             const bool gt = !std::strcmp(flag, "MK_FLAG_GT"), lt = !std::strcmp(flag, "MK_FLAG_LT");
-            if (!fmin && g.lim->sat_count && g.lim->sat_dec == 1 && ((gt && step <= -2) || (lt && step >= 1))) {
+            if (!fmin && g.lim->sat_count && (g.lim->sat_dec == 1 || g.lim->sat_dec == 3) &&
+                ((gt && step <= -2) || (lt && step >= 1))) {
                 // Counter form (MK_JIT_SAT_COUNT, round 4): a countdown by k
                 // (x > 0, x -= k; or x < 0, x += k) from x1 after the first
                 // iteration runs z = ceil(|x1| / k) more iterations, so each
@@ -1550,7 +1551,10 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 e.line("    more = MK_KEEP(z != 0, need);");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
-                for (int u = 0; u < uf; ++u) e.line("    z = MK_SATDEC(z);");
+                if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0) // sat_block decrements per asm block
+                    for (int u = 0; u < uf; u += (int)g.lim->sat_block) e.line("    z = MK_SATDECB(z);");
+                else
+                    for (int u = 0; u < uf; ++u) e.line("    z = MK_SATDEC(z);");
                 e.line("    more = MK_KEEP(z != 0, need);");
                 e.line("    }");
                 e.line("    a = z != 0;");
@@ -1569,8 +1573,11 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 e.line("    more = MK_KEEP(x != 0, need);");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
-                for (int u = 0; u < uf; ++u)
-                    e.line(g.lim->sat_dec == 2 ? "    x = MK_SATSUB(x, one_);" : "    x = MK_SATDEC(x);");
+                if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0)
+                    for (int u = 0; u < uf; u += (int)g.lim->sat_block) e.line("    x = MK_SATDECB(x);");
+                else
+                    for (int u = 0; u < uf; ++u)
+                        e.line(g.lim->sat_dec == 2 ? "    x = MK_SATSUB(x, one_);" : "    x = MK_SATDEC(x);");
                 e.line("    more = MK_KEEP(x != 0, need);");
                 e.line("    }");
                 e.line("    a = x != 0;");
@@ -1665,6 +1672,12 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     std::vector<uint32_t> loops;
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 1");
+    if (g.lim->sat_dec == 3) { // host builds: sat_block plain decrements (the device prelude's asm block wins)
+        e.line("#ifndef MK_SATDECB");
+        e.line("#define MK_SATDECB(x) ([](int32_t v_) { for (int k_ = 0; k_ < %u; ++k_) v_ = MK_SATDEC(v_); return v_; }(x))",
+               g.lim->sat_block);
+        e.line("#endif");
+    }
     e.line("#ifndef MK_CTABLE");
     e.line("#define MK_CTABLE static const");
     e.line("#endif");
@@ -2691,6 +2704,8 @@ JitLimits JitLimits::from_env()
     }
     flag("MK_JIT_FLAG_MIN", l.flag_min);
     num("MK_JIT_SAT_DEC", l.sat_dec);
+    num("MK_JIT_SAT_BLOCK", l.sat_block);
+    if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_TS_WAVE", l.ts_wave);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
@@ -2725,6 +2740,7 @@ std::string JitLimits::key() const
     if (prof) k += ",prof=1";
     if (lin_sum) k += ",lsum=1";
     if (chain) k += ",chain=1";
+    if (sat_dec == 3) k += ",sblk=" + std::to_string(sat_block);
     return k;
 }
 
@@ -3090,6 +3106,16 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
         // x - 1 saturating at 0 as unsigned (asm: LLVM folds a chain of them into one subtract)
         e.line("MK_FN int32_t mk_satdec(int32_t x) { int32_t r; __asm__(\"v_sub_u32_e64 %%0, %%1, 1 clamp\" : \"=v\"(r) : \"v\"(x)); return r; }");
         e.line("#define MK_SATDEC(x) mk_satdec(x)");
+        // sat_block of them in one asm statement: the hazard recognizer's
+        // s_nop after an asm statement then comes once per block
+        // (MK_JIT_SAT_DEC=3, MK_JIT_SAT_BLOCK)
+        if (lim.sat_dec == 3) {
+            std::string b = "MK_FN int32_t mk_satdecb(int32_t x) { __asm__(\"";
+            for (uint32_t k = 0; k < lim.sat_block; ++k) b += k ? "\\n\\tv_sub_u32_e64 %0, %0, 1 clamp" : "v_sub_u32_e64 %0, %0, 1 clamp";
+            b += "\" : \"+v\"(x)); return x; }\n";
+            e.s += b;
+        }
+        e.line("#define MK_SATDECB(x) mk_satdecb(x)");
         // the same in plain C, by a 1 that LLVM cannot see (no hazard s_nop after asm)
         e.line("MK_FN uint32_t mk_opaque1() { uint32_t r; __asm__(\"v_mov_b32 %%0, 1\" : \"=v\"(r)); return r; }");
         e.line("#define MK_OPAQUE1() mk_opaque1()");

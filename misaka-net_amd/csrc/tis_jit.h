@@ -136,7 +136,12 @@ struct JitLimits {
     // iteration (v_sub_u32 x, x, 1 clamp: a lane that left holds 0), the
     // flag being x != 0 (MK_JIT_SAT_DEC=0: sub + min_u32 per iteration;
     // 1: inline asm; 2: LLVM's usub.sat by an opaque 1, no hazard s_nop).
-    uint32_t sat_dec = 1;
+    // 3 (default since round 4): as 1 with MK_JIT_SAT_BLOCK (4, 8, 16, 32)
+    // decrements per asm statement, so the hazard recognizer's s_nop after an
+    // asm statement comes once per block (r05h, C5 launch: block 4 120.6 us,
+    // 8 121.9, 16 121.6, 32 122.9, one per statement 125.2-125.6).
+    uint32_t sat_dec = 3;
+    uint32_t sat_block = 4;
     // ... and a countdown by any other step k (x > 0, x -= k; x < 0, x += k)
     // as one saturating decrement of its remaining-iteration count per
     // iteration (MK_JIT_SAT_COUNT=0: the bump and a med3 / shift flag).

@@ -146,10 +146,12 @@ def test_loop_phases(tmp_path):
 # counter form of countdowns by other steps (MK_JIT_SAT_COUNT, default on;
 # "count0" turns it off): every loop path, and C5 over all trip counts and at
 # budgets inside its loops.
-@pytest.mark.parametrize("mode", ["0", "2", "count0", "default"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "count0", "b8", "b32", "default"])
 def test_countdown_forms(tmp_path, monkeypatch, mode):
     if mode == "count0":
         monkeypatch.setenv("MK_JIT_SAT_COUNT", "0")
+    elif mode.startswith("b"):  # the default form (3) with other asm block sizes
+        monkeypatch.setenv("MK_JIT_SAT_BLOCK", mode[1:])
     elif mode != "default":
         monkeypatch.setenv("MK_JIT_SAT_DEC", mode)
     cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
