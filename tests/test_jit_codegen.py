@@ -146,7 +146,7 @@ def test_loop_phases(tmp_path):
 # counter form of countdowns by other steps (MK_JIT_SAT_COUNT, default on;
 # "count0" turns it off): every loop path, and C5 over all trip counts and at
 # budgets inside its loops.
-@pytest.mark.parametrize("mode", ["0", "1", "2", "count0", "b8", "b32", "default"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "count0", "b32", "default"])
 def test_countdown_forms(tmp_path, monkeypatch, mode):
     if mode == "count0":
         monkeypatch.setenv("MK_JIT_SAT_COUNT", "0")

@@ -157,7 +157,7 @@ t = time.time()
 small = mk.Network(mk.networks.example_network()).plan()
 print("RESULT", big.split()[0], small.split()[0], round(time.time() - t, 2), flush=True)
 """
-    e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_COMPILE_S="2", AMD_COMGR_CACHE="0")
+    e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_COMPILE_S="2", AMD_COMGR_CACHE="0", MK_JIT_TUNE_REGS="0")
     r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True, timeout=600,
                        env=e)
     assert r.returncode == 0, r.stderr[-3000:]
