@@ -3071,6 +3071,9 @@ struct mk_session {
     // native tier (tis_jit.h mk_sess_exec): the session schedule compiled to
     // a kernel; the interpreter's state above holds the sessions handed to it
     bool native = false;
+    // longest call on the native tier (jit_session_max_call_steps): with a
+    // budget above it no call hands off, and the interpreter is not launched
+    uint64_t call_steps = UINT64_MAX;
     std::string plan; // mk_session_plan
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
@@ -3155,6 +3158,9 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
         p.fuse_import = 1u;
         p.imp = SessImport{s->n, s->nprog, s->nstack, s->nsb, s->sflags, s->epoch, s->hand_sb, s->hand_steps,
                            s->regs, s->slots, s->hdr, s->rec, s->dyn_base};
+        // no call of this network can reach the budget: none hands off and
+        // the interpreter holds no session, so its pass would only exit
+        if (s->call_steps < (uint64_t)p.budget && !std::getenv("MK_SESS_ALWAYS_INTERP")) return MK_OK;
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
@@ -3234,6 +3240,7 @@ int session_native(mk_session *s)
         return MK_EDEVICE;
     s->native_bytes = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5] + sz[6]; // the lane state: what a reset clears
     s->native = true;
+    s->call_steps = jit_session_max_call_steps(P, h->jit_lim);
     s->p.nsb = s->nsb;
     s->p.hand_call = s->hand_call;
     s->p.sflags = s->sflags;
@@ -3246,6 +3253,9 @@ int session_native(mk_session *s)
              "compile=%.2fs rtc=%s state_regs=%zu", P.nsb, P.nregs, P.nslots, P.code.size(), src.size(),
              (unsigned long long)src_hash(src), secs, from.c_str(), live_regs);
     s->plan = line;
+    // calls that cannot reach the budget: one launch per call (no interpreter pass)
+    s->plan += s->call_steps < (uint64_t)s->p.budget ? " call_steps=" + std::to_string(s->call_steps) + " launches=1"
+                                                     : std::string(" launches=2");
     return MK_OK;
 }
 

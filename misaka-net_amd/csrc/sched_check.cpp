@@ -439,6 +439,19 @@ int mkc_sess_lane(void *hv, uint32_t cap, uint32_t *nregs, uint32_t *nslots, cha
     return rc;
 }
 
+// The longest call of the session schedule (tis_jit.h
+// jit_session_max_call_steps; UINT64_MAX: unbounded): 0, or 1 when the
+// session compiler declined.
+int mkc_sess_call_steps(void *hv, uint32_t cap, uint64_t *out)
+{
+    auto *h = (CheckNet *)hv;
+    mk::SchedProgram P;
+    std::string w;
+    if (!mk::compile_session_schedule(h->net, cap, mk::SchedLimits{}, P, w)) return 1;
+    *out = mk::jit_session_max_call_steps(P, mk::JitLimits::from_env());
+    return 0;
+}
+
 // The whole session module (lane + mk_sess_exec) as hiprtc gets it.
 int mkc_sess_module(void *hv, uint32_t cap, char *out, size_t out_len)
 {

@@ -3270,6 +3270,84 @@ bool jit_session_source(const SchedProgram &p, const JitLimits &lim, std::string
     return true;
 }
 
+// The most node-instructions one /compute call can retire on the session
+// schedule's fast variants: the longest path from a call's entry (variant 0,
+// or where a U_YIELD sends the next call) to the U_YIELD or U_END that ends
+// it; UINT64_MAX when a call can loop (a cycle between yields) or the
+// schedule does not analyze.  A launch whose budget exceeds it never fires a
+// budget guard, so no call hands off to the interpreter (round 4).
+uint64_t jit_session_max_call_steps(const SchedProgram &p, const JitLimits &lim)
+{
+    if (!p.session) return UINT64_MAX;
+    Graph g;
+    std::string why;
+    if (!analyze(p, lim, g, why)) return UINT64_MAX;
+    const size_t nv = g.entry.size();
+    // successors through the fast variant's exits, with the steps retired on
+    // the way to each; a call ends at U_YIELD / U_END (its steps in `fin`)
+    auto exits = [&](uint32_t v, std::vector<std::pair<uint32_t, uint64_t>> &succ, uint64_t &fin,
+                     uint32_t &next) -> bool {
+        succ.clear();
+        fin = 0;
+        next = ~0u;
+        for (size_t pc = g.entry[v];; ++pc) {
+            const DOp &I = g.D[pc];
+            switch (I.op) {
+            case U_GUARD: continue; // not taken when the budget exceeds every path
+            case U_BRX: succ.push_back({(uint32_t)I.imm, I.inc}); continue;
+            case U_JUMP: succ.push_back({(uint32_t)I.imm, I.inc}); return true;
+            case U_BR:
+                succ.push_back({(uint32_t)(uint64_t)I.imm, I.inc});
+                succ.push_back({(uint32_t)((uint64_t)I.imm >> 32), I.inc});
+                return true;
+            case U_JRO:
+                for (uint64_t t = 0; t <= I.b; ++t) succ.push_back({p.jtab[(size_t)I.imm + t], I.inc});
+                return true;
+            case U_OVF: fin = std::max<uint64_t>(fin, I.inc); continue; // a full dynamic stack ends the session here
+            case U_YIELD: fin = std::max<uint64_t>(fin, I.inc); next = (uint32_t)(uint64_t)I.imm; return true;
+            case U_END: fin = std::max<uint64_t>(fin, I.inc); return true;
+            case U_HANDOFF: return false; // (only in checked variants, which the fast paths do not reach)
+            default:
+                if (I.op > U_DATA_LAST && I.op != U_ROUND_END) return false; // unknown control: no bound
+                continue;
+            }
+        }
+    };
+    std::vector<int64_t> memo(nv, -1);
+    std::vector<uint8_t> state(nv, 0);
+    std::vector<uint32_t> roots{0u};
+    std::vector<std::pair<uint32_t, uint64_t>> succ;
+    uint64_t fin = 0, best_all = 0;
+    uint32_t next = 0;
+    for (size_t r = 0; r < roots.size(); ++r) {
+        std::vector<uint32_t> stack{roots[r]};
+        while (!stack.empty()) {
+            const uint32_t v = stack.back();
+            if (v >= nv) return UINT64_MAX;
+            if (state[v] == 0) {
+                state[v] = 1;
+                if (!exits(v, succ, fin, next)) return UINT64_MAX;
+                if (next != ~0u && std::find(roots.begin(), roots.end(), next) == roots.end()) roots.push_back(next);
+                for (const auto &w : succ) {
+                    if (w.first >= nv) return UINT64_MAX;
+                    if (state[w.first] == 1) return UINT64_MAX; // a cycle inside a call
+                    if (state[w.first] == 0) stack.push_back(w.first);
+                }
+                continue;
+            }
+            stack.pop_back();
+            if (state[v] == 2) continue;
+            (void)exits(v, succ, fin, next);
+            int64_t best = (int64_t)fin;
+            for (const auto &w : succ) best = std::max<int64_t>(best, (int64_t)w.second + memo[w.first]);
+            memo[v] = best;
+            state[v] = 2;
+        }
+        best_all = std::max<uint64_t>(best_all, (uint64_t)memo[roots[r]]);
+    }
+    return best_all;
+}
+
 bool jit_session_lane(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why)
 {
     if (!p.session) {

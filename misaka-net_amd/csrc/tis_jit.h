@@ -259,6 +259,9 @@ constexpr uint32_t kJitWaveBlockedSlots = 1u << 22;
 // session, state in HBM; handed-off calls go to the interpreter.
 constexpr const char *kJitSessKernel = "mk_sess_exec";
 bool jit_session_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why);
+// Longest call of a session schedule in retired node-instructions
+// (UINT64_MAX: unbounded, a call can loop); see tis_jit.cpp.
+uint64_t jit_session_max_call_steps(const SchedProgram &p, const JitLimits &lim);
 // The lane part alone (CPU tests compile it with g++).
 bool jit_session_lane(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why);
 

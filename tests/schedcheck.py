@@ -192,6 +192,21 @@ def session_lane(nodes, *, stack_cap=None):
         lib().mkc_free(h)
 
 
+def session_max_call_steps(nodes, *, stack_cap=None):
+    """Longest /compute call of the session schedule (None: unbounded)."""
+    h, _keep = _load(nodes)
+    try:
+        lib().mkc_sess_call_steps.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+        v = C.c_uint64()
+        rc = lib().mkc_sess_call_steps(h, 1024 if stack_cap is None else stack_cap, C.byref(v))
+        if rc == 1:
+            raise NotCompiled("session schedule declined")
+        assert rc == 0, rc
+        return None if v.value == (1 << 64) - 1 else v.value
+    finally:
+        lib().mkc_free(h)
+
+
 def session_module(nodes, *, stack_cap=None):
     """The native session module's full source (what hiprtc compiles)."""
     h, _keep = _load(nodes)

@@ -15,6 +15,7 @@ import pytest
 
 import misaka_net_amd as mk
 from oracle import pyoracle as po
+import schedcheck as sc
 from schedcheck import HANDOFF, HostSessions, NotCompiled
 from tisgen import random_network, stack_loop_network
 
@@ -247,3 +248,32 @@ def test_session_modules_compile_for_gfx950(tmp_path):
         r = subprocess.run([rtc, str(p), str(tmp_path / f"{name}.co")], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, (name, r.stdout[-2000:])
         assert (tmp_path / f"{name}.co").stat().st_size > 0
+
+
+def test_session_call_bound_covers_every_call():
+    """jit_session_max_call_steps (tis_jit.cpp): a network whose calls cannot
+    loop gets a bound on any call's retired steps, which the session
+    launches use to skip the interpreter pass (no call can hand off below
+    it).  Every emulated call -- sequential calls on 64 instances, full-range
+    inputs -- retires at most the bound; networks with data-dependent loops
+    are unbounded."""
+    bounded = {"example": mk.networks.example_network(), "sample": mk.networks.sample_network(),
+               "pipeline4": mk.networks.pipeline_network(4)}
+    for seed in range(12):
+        bounded[f"rand{seed}"] = random_network(seed)
+    seen_bounded = 0
+    for name, nodes in bounded.items():
+        try:
+            bound = sc.session_max_call_steps(nodes)
+        except sc.NotCompiled:
+            continue
+        if bound is None:
+            continue
+        seen_bounded += 1
+        emu = sc.HostSessions(nodes, 64)
+        for call in range(6):
+            _, _, sp = emu.call(po.gen_inputs(0x4D49534B41 + call, 64))
+            assert int(sp.max()) <= bound, (name, call, int(sp.max()), bound)
+    assert seen_bounded >= 3
+    assert sc.session_max_call_steps(mk.networks.countdown_network()) is None
+    assert sc.session_max_call_steps(mk.networks.example_network()) is not None
