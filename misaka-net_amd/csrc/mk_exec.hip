@@ -3160,7 +3160,12 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
                            s->regs, s->slots, s->hdr, s->rec, s->dyn_base};
         // no call of this network can reach the budget: none hands off and
         // the interpreter holds no session, so its pass would only exit
-        if (s->call_steps < (uint64_t)p.budget && !std::getenv("MK_SESS_ALWAYS_INTERP")) return MK_OK;
+        // (MK_SESS_ALWAYS_INTERP=1 launches it anyway: A/B runs)
+        static const bool always = [] {
+            const char *e = std::getenv("MK_SESS_ALWAYS_INTERP");
+            return e && *e == '1';
+        }();
+        if (s->call_steps < (uint64_t)p.budget && !always) return MK_OK;
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
