@@ -1494,6 +1494,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("        break;");
     e.line("    }");
     e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
+    if (g.lim->prio) e.line("    MK_PRIO_LOOP();");
     e.line("    bool a = true, more = true;");
     if (ovf) {
         e.line("    bool ovf_ = false, brx_ = false;");
@@ -1623,6 +1624,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     for (int u = 0; u < kLoopUnroll; ++u) iteration(LOOP_GUARDED);
     e.line("    } while (MK_KEEP(a, need));");
     e.line("    }");
+    if (g.lim->prio) e.line("    MK_PRIO_REST();");
     // a: still in the loop (suspended); otherwise it left through the branch
     // (the condition on its frozen registers fails) or through the guard
     if (brx) {
@@ -1672,6 +1674,12 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     std::vector<uint32_t> loops;
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 1");
+    if (g.lim->prio) { // wave priority around self-loops (MK_JIT_PRIO, the module header); none in host builds
+        e.line("#ifndef MK_PRIO_LOOP");
+        e.line("#define MK_PRIO_LOOP()");
+        e.line("#define MK_PRIO_REST()");
+        e.line("#endif");
+    }
     if (g.lim->sat_dec == 3) { // host builds: sat_block plain decrements (the device prelude's asm block wins)
         e.line("#ifndef MK_SATDECB");
         e.line("#define MK_SATDECB(x) ([](int32_t v_) { for (int k_ = 0; k_ < %u; ++k_) v_ = MK_SATDEC(v_); return v_; }(x))",
@@ -2718,6 +2726,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_PROF", l.prof);
     flag("MK_JIT_LIN_SUM", l.lin_sum);
     flag("MK_JIT_CHAIN", l.chain);
+    flag("MK_JIT_PRIO", l.prio);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2740,6 +2749,7 @@ std::string JitLimits::key() const
     if (prof) k += ",prof=1";
     if (lin_sum) k += ",lsum=1";
     if (chain) k += ",chain=1";
+    if (!prio) k += ",prio=0";
     if (sat_dec == 3) k += ",sblk=" + std::to_string(sat_block);
     return k;
 }
@@ -3075,6 +3085,14 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     }
     if (lim.ts_wave) e.line("#define MK_WS_R 12u"); // kMachineWaveSortKernel: a wave's tile, inputs per lane
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
+    // MK_JIT_PRIO=1: waves in a self-loop's phases at priority 0, after a
+    // loop (dispatch rounds, latency-bound) at 1, so the issue arbiter
+    // prefers them over the loops' throughput-bound VALU streams (a wave
+    // starts at 0)
+    if (lim.prio && shape == JIT_MACHINE) {
+        e.line("#define MK_PRIO_LOOP() __builtin_amdgcn_s_setprio(0)");
+        e.line("#define MK_PRIO_REST() __builtin_amdgcn_s_setprio(1)");
+    }
     // the machine lane's dispatch value as an SGPR value GVN cannot equate
     // with the lane's superblock id (MK_SCALAR, chosen by emit_machine_lane;
     // machine modules only, so the stream modules' sources stay as they were)

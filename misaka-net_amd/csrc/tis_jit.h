@@ -190,6 +190,11 @@ struct JitLimits {
     // vs 132.9 -- the extra paths cost more than the dispatch rounds saved.
     // Off.
     bool chain = false;
+    // Wave priority: 0 inside self-loops, 1 after them (module_prelude;
+    // MK_JIT_PRIO=0: none).  The issue arbiter then prefers the dispatch
+    // rounds' latency-bound waves over the loops' VALU streams (r05o, C5
+    // launch 120.6 / 121.1 -> 111.7 / 111.6 us).
+    bool prio = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
