@@ -1479,6 +1479,22 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     };
     int uf = fast_unroll(xpc - gpc - 1);
     if (g.lim->loop_unroll >= 1 && g.lim->loop_unroll <= 64) uf = g.lim->loop_unroll; // MK_JIT_LOOP_UNROLL
+    // Saturating countdowns (counter c >= 0 per lane, 0 once it left): chunks
+    // of 2 uf decrements while some lane still needs more than uf, then the
+    // uf chunks -- half the exit tests on long trips, and no more idle
+    // iterations than uf chunks alone (a 2 uf chunk starts only when a lane
+    // needs over uf of them).  MK_JIT_SAT_TIER=0: uf chunks only.
+    auto emit_sat_tier = [&](const char *c) {
+        if (!g.lim->sat_tier) return;
+        e.line("    while (more && T32 - it >= %uu && MK_KEEP(%s > %d, need)) {", 2 * uf, c, uf);
+        e.line("    it += %uu;", 2 * uf);
+        if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0)
+            for (int u = 0; u < 2 * uf; u += (int)g.lim->sat_block) e.line("    %s = MK_SATDECB(%s);", c, c);
+        else
+            for (int u = 0; u < 2 * uf; ++u) e.line("    %s = MK_SATDEC(%s);", c, c);
+        e.line("    }");
+        e.line("    more = MK_KEEP(%s != 0, need);", c);
+    };
     // an unguarded phase: chunks of uf iterations while T allows
     auto phase = [&](LoopMode mode, const char *cap) {
         e.line("    while (more && %s - it >= %uu) {", cap, uf);
@@ -1550,6 +1566,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                        (unsigned long long)(k - 1), (unsigned long long)k);
                 e.line("    int32_t z = (int32_t)z0;");
                 e.line("    more = MK_KEEP(z != 0, need);");
+                emit_sat_tier("z");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
                 if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0) // sat_block decrements per asm block
@@ -1572,6 +1589,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 e.line("    x = f0 ? x : 0;");
                 if (g.lim->sat_dec == 2) e.line("    const uint32_t one_ = MK_OPAQUE1();");
                 e.line("    more = MK_KEEP(x != 0, need);");
+                if (g.lim->sat_dec != 2) emit_sat_tier("x");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
                 if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0)
@@ -2727,6 +2745,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_LIN_SUM", l.lin_sum);
     flag("MK_JIT_CHAIN", l.chain);
     flag("MK_JIT_PRIO", l.prio);
+    flag("MK_JIT_SAT_TIER", l.sat_tier);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2750,6 +2769,7 @@ std::string JitLimits::key() const
     if (lin_sum) k += ",lsum=1";
     if (chain) k += ",chain=1";
     if (!prio) k += ",prio=0";
+    if (sat_tier) k += ",stier=1";
     if (sat_dec == 3) k += ",sblk=" + std::to_string(sat_block);
     return k;
 }

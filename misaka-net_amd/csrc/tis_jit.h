@@ -195,6 +195,9 @@ struct JitLimits {
     // rounds' latency-bound waves over the loops' VALU streams (r05o, C5
     // launch 120.6 / 121.1 -> 111.7 / 111.6 us).
     bool prio = true;
+    // Saturating countdowns run chunks of twice the unroll while some lane
+    // still needs more than one unroll (emit_self_loop; MK_JIT_SAT_TIER=1).
+    bool sat_tier = false;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
