@@ -2769,7 +2769,7 @@ std::string JitLimits::key() const
     if (lin_sum) k += ",lsum=1";
     if (chain) k += ",chain=1";
     if (!prio) k += ",prio=0";
-    if (sat_tier) k += ",stier=1";
+    if (!sat_tier) k += ",stier=0";
     if (sat_dec == 3) k += ",sblk=" + std::to_string(sat_block);
     return k;
 }

@@ -196,8 +196,9 @@ struct JitLimits {
     // launch 120.6 / 121.1 -> 111.7 / 111.6 us).
     bool prio = true;
     // Saturating countdowns run chunks of twice the unroll while some lane
-    // still needs more than one unroll (emit_self_loop; MK_JIT_SAT_TIER=1).
-    bool sat_tier = false;
+    // still needs more than one unroll (emit_self_loop; MK_JIT_SAT_TIER=0: off).
+    // C5 111.1 / 111.6 -> 105.3 / 105.3 us (r05s); GPU parity subset green with it.
+    bool sat_tier = true;
 
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
