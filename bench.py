@@ -4,10 +4,17 @@
 One "step" = one pass of the executor over one batch of synthetic /compute
 inputs already resident in HBM (BASELINE.json config 2 by default: the
 docker-compose example network, 16,777,216 lanes per GPU).  With --gpus N
-(launched by torch.distributed.run, one process per GPU) every rank runs its
-own contiguous shard of global lane indices -- weak scaling, no data-path
-collective; RCCL carries only the final counter reduction (and the optional
-ordered output gather, --gather, timed separately).
+every rank (one process per GPU) runs its own contiguous shard of global lane
+indices -- weak scaling, no data-path collective; RCCL carries only the final
+counter reduction and the ordered output gather to rank 0 (`end_to_end`,
+timed separately and verified against one launch over every global lane).
+
+Ranks: under torch.distributed.run each process is one rank.  A bare
+`python bench.py --gpus N` (N > 1, WORLD_SIZE unset) starts its own N child
+ranks first -- fresh processes with the launcher's RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* variables, started before anything loads the executor
+or touches a GPU (misaka_net_amd.dist.launch_ranks) -- forwards rank 0's
+line and exits non-zero if any rank fails.
 
 Prints ONE JSON line on rank 0 (keys per the driver contract + roofline +
 cpu_baseline).
@@ -21,11 +28,27 @@ import re
 import sys
 import time
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _gpus_arg(argv) -> int:
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=1)
+    return p.parse_known_args(argv)[0].gpus
+
+
+if __name__ == "__main__":
+    # importing the package loads no library and touches no GPU (the ctypes
+    # binding loads libmisaka_amd.so on first use): the parent stays GPU-free
+    from misaka_net_amd import dist as _mkdist
+
+    _n = _gpus_arg(sys.argv[1:])
+    if _mkdist.needs_launch(_n, os.environ):
+        sys.exit(_mkdist.launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], _n))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 import misaka_net_amd as mk  # noqa: E402
 from misaka_net_amd import _native as N  # noqa: E402
@@ -366,8 +389,10 @@ def main():
     ap.add_argument("--http", type=int, default=0, metavar="CLIENTS",
                     help="also time single-value /compute requests through the HTTP master with this many "
                          "concurrent keep-alive clients (reported as http, never as value)")
-    ap.add_argument("--verify-gather", action="store_true",
-                    help="N > 1: rank 0 checks the gathered outputs against one launch over every global lane")
+    ap.add_argument("--no-verify-gather", dest="verify_gather", action="store_false",
+                    help="N > 1: skip rank 0's check of the gathered outputs against one launch over every "
+                         "global lane (on by default)")
+    ap.add_argument("--verify-gather", dest="verify_gather", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--refstruct-seconds", type=float, default=5.0,
                     help="sample length of the reference-structured CPU emulation (0: skip)")
     args = ap.parse_args()
@@ -379,6 +404,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if not args.same_device and world > 1 and local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) visible "
+                         "(--same-device rehearses N ranks on one GPU)")
     dist = None
     if args.same_device:  # rehearsal of the N-rank path on a one-GPU box
         local = 0

@@ -33,8 +33,7 @@
 #include <ucontext.h>
 #include <sys/syscall.h>
 #include <signal.h>
-#include <spawn.h>
-#include <sys/wait.h>
+#include <glob.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -1535,7 +1534,7 @@ struct JitState {
     bool heavy = false;              // stream shape, one lane per thread (kStreamKernelHeavy)
     bool lds = false;                // heavy kernel with all its stack slots in LDS (no HBM slots)
     uint32_t lds_n = 0;              // heavy kernel: slots per lane in LDS (the rest in HBM)
-    std::string rtc;                 // compiler of the module: linked / ns / helper / linked-other
+    std::string rtc;                 // compiler of the module: linked / ns / linked-other
     uint32_t pool = 0;               // machine shape: lane-pool slots per wave (kMachinePoolKernel)
     int block = kJitBlock;
     JitDev dev[kMaxDevices];
@@ -1579,26 +1578,17 @@ struct DevCtx {
     hipEvent_t ev = nullptr;
 };
 
-// Native modules loaded once per (device, code object) and never unloaded:
-// MK_JIT_KEEP_MODULES=1 for every module, =0 for none; unset, the modules a
-// helper process compiled (ROCm 7.2 code objects run by PyTorch's bundled
-// runtime) when kKeepHelperModules.  Networks and sessions
-// whose code objects are equal share one module.
-constexpr bool kKeepHelperModules = false;
-
-inline int keep_policy() // 1 all, 0 none, -1 by compiler
+// Native modules loaded once per (device, code object) and never unloaded
+// with MK_JIT_KEEP_MODULES=1 (diagnostics); by default each network unloads
+// its own.  Networks and sessions whose code objects are equal share one
+// kept module.
+inline bool keep_module(const std::string &)
 {
-    static const int k = [] {
+    static const bool k = [] {
         const char *s = std::getenv("MK_JIT_KEEP_MODULES");
-        return s && *s ? (*s == '1' ? 1 : 0) : -1;
+        return s && *s == '1';
     }();
     return k;
-}
-
-inline bool keep_module(const std::string &from)
-{
-    const int k = keep_policy();
-    return k == 1 || (k < 0 && kKeepHelperModules && from == "helper");
 }
 
 struct KeptModule {
@@ -2109,17 +2099,17 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
 }
 
 // ---- tier 3: native kernel per schedule (tis_jit.h) ------------------------
-// One hiprtc compilation, run on a helper thread so that the caller can give
-// up after lim.max_compile_s: the job owns its inputs and outputs (shared),
-// so a compile the caller abandoned finishes in the background and is
-// discarded (a helper child process is killed at once).
+// One hiprtc compilation, run on a compile thread so that the caller can
+// give up after lim.max_compile_s: the job owns its inputs and outputs
+// (shared), so a compile the caller abandoned finishes in the background and
+// is discarded.
 struct HiprtcJob {
     std::string src;
+    std::vector<std::string> env; // the caller's environment, copied on the caller's thread (rtc_compile)
     std::mutex mu;
     std::condition_variable cv;
     bool done = false, ok = false;
     bool abandoned = false; // the caller gave up (under mu)
-    pid_t pid = 0;          // the helper child while it runs (under mu)
     std::string why;
     std::vector<char> code;
 };
@@ -2266,21 +2256,22 @@ struct RtcDrain {
 // the process), and the module is compiled in process by that copy, so
 // every caller gets the same module without a child process.
 //
-// Round 3 compiled such modules in a child process (mk_rtc, posix_spawn from
-// a compile thread); the host heap of those PyTorch processes was found
-// corrupted at exit.  The helper stays available by name only
-// (MK_HIPRTC=helper, or MK_HIPRTC=<path of a helper>); MK_HIPRTC=linked
+// Round 3 compiled such modules in a child process (posix_spawn from a
+// compile thread of a GPU-initialised process); the host heap of those
+// PyTorch processes was found corrupted at exit.  Round 5
+// removed that path: this library starts no process.  MK_HIPRTC=linked
 // compiles with whatever hiprtc the process resolved (PyTorch's in a PyTorch
-// process).
+// process), MK_HIPRTC=ns with the namespace copy; any other value is refused
+// (the network stays on tier 2, the plan says why).
 #ifndef MK_ROCM_LIB
 #define MK_ROCM_LIB "/opt/rocm/lib"
 #endif
 
-enum RtcKind { RTC_LINKED, RTC_NS, RTC_HELPER };
+enum RtcKind { RTC_LINKED, RTC_NS, RTC_REFUSED };
 
 struct RtcChoice {
     RtcKind kind = RTC_LINKED;
-    std::string helper; // RTC_HELPER: the executable
+    std::string why; // RTC_REFUSED: the reason
 };
 
 // Whether the linked hiprtc is another install's than this ROCm's (PyTorch's
@@ -2305,18 +2296,8 @@ RtcChoice rtc_choice()
             c.kind = RTC_NS;
             return c;
         }
-        c.kind = RTC_HELPER;
-        if (std::strcmp(e, "helper")) {
-            c.helper = e;
-            return c;
-        }
-        Dl_info info{};
-        if (dladdr(reinterpret_cast<void *>(&rtc_choice), &info) && info.dli_fname) {
-            std::string dir(info.dli_fname);
-            const size_t slash = dir.rfind('/');
-            dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
-            if (access((dir + "/mk_rtc").c_str(), X_OK) == 0) c.helper = dir + "/mk_rtc";
-        }
+        c.kind = RTC_REFUSED; // the round-3 helper process (=helper / =<path>) was removed
+        c.why = std::string("MK_HIPRTC=") + e + " refused: only linked and ns compile (no helper process)";
         return c;
     }
     if (inproc_rtc_differs()) c.kind = RTC_NS;
@@ -2348,6 +2329,23 @@ void rtc_drain_at_exit();
 // Namespaces the compiler may open: one per compile worker (NsPool).
 constexpr size_t kNsMax = 4;
 
+// This ROCm's libhiprtc: the versioned sonames under MK_ROCM_LIB, highest
+// first (libhiprtc.so.7 on ROCm 7.x), then the unversioned link.
+std::vector<std::string> hiprtc_candidates()
+{
+    std::vector<std::string> v;
+    glob_t g{};
+    if (glob(MK_ROCM_LIB "/libhiprtc.so.[0-9]*", 0, nullptr, &g) == 0)
+        for (size_t i = 0; i < g.gl_pathc; i++) v.emplace_back(g.gl_pathv[i]);
+    globfree(&g);
+    // libhiprtc.so.7 before libhiprtc.so.7.2.x: the soname before the file
+    std::sort(v.begin(), v.end(), [](const std::string &a, const std::string &b) {
+        return a.size() != b.size() ? a.size() < b.size() : a > b;
+    });
+    v.emplace_back(MK_ROCM_LIB "/libhiprtc.so");
+    return v;
+}
+
 // This ROCm's hiprtc in namespace k, opened on first use (by worker k's
 // thread, see NsCompiler).
 const RtcApi *ns_rtc(size_t k, std::string &why)
@@ -2356,10 +2354,15 @@ const RtcApi *ns_rtc(size_t k, std::string &why)
     static const RtcApi *api[kNsMax];
     static std::once_flag once[kNsMax];
     std::call_once(once[k], [k] { api[k] = [k]() -> const RtcApi * {
-        void *h = dlmopen(LM_ID_NEWLM, MK_ROCM_LIB "/libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
-        if (!h) {
+        void *h = nullptr;
+        std::string errs;
+        for (const std::string &path : hiprtc_candidates()) {
+            if ((h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
             const char *d = dlerror();
-            fail[k] = std::string("dlmopen: ") + (d ? d : "failed");
+            errs += (errs.empty() ? "" : "; ") + std::string(d ? d : path + ": failed");
+        }
+        if (!h) {
+            fail[k] = "dlmopen: " + errs;
             return nullptr;
         }
         auto *a = new RtcApi{};
@@ -2518,65 +2521,7 @@ bool write_file(const std::string &path, const std::string &data)
     return close(fd) == 0 && off == data.size();
 }
 
-std::string read_file(const std::string &path, size_t max = SIZE_MAX)
-{
-    std::ifstream f(path, std::ios::binary);
-    std::string d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-    return d.size() > max ? d.substr(0, max) : d;
-}
-
-// Compile with the helper process, its files in a private directory
-// (mkdtemp, 0700).  Returns false (nothing learned) when the helper could
-// not run; `ok` tells whether it compiled.
-bool rtc_spawn(const std::string &helper, HiprtcJob &j, bool &ok, std::string &why, std::vector<char> &code)
-{
-    const char *td = std::getenv("TMPDIR");
-    std::string base = std::string(td && *td ? td : "/tmp") + "/mk_rtc_XXXXXX";
-    std::vector<char> tmpl(base.begin(), base.end());
-    tmpl.push_back('\0');
-    if (!mkdtemp(tmpl.data())) return false;
-    const std::string dir(tmpl.data()), in = dir + "/lane.hip", out = dir + "/lane.co", log = dir + "/log";
-    bool ran = false;
-    if (write_file(in, j.src)) {
-        posix_spawn_file_actions_t fa;
-        posix_spawn_file_actions_init(&fa);
-        posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0600);
-        posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
-        char *argv[] = {const_cast<char *>(helper.c_str()), const_cast<char *>(in.c_str()),
-                        const_cast<char *>(out.c_str()), nullptr};
-        pid_t pid = 0;
-        std::unique_lock<std::mutex> lk(j.mu);
-        if (!j.abandoned && posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv, environ) == 0) {
-            j.pid = pid;
-            lk.unlock();
-            int st = 0;
-            while (waitpid(pid, &st, 0) < 0 && errno == EINTR) {
-            }
-            lk.lock();
-            j.pid = 0;
-            lk.unlock();
-            ran = WIFEXITED(st) && (WEXITSTATUS(st) == 0 || WEXITSTATUS(st) == 1);
-            ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
-            if (ok) {
-                const std::string c = read_file(out);
-                code.assign(c.begin(), c.end());
-                ok = !code.empty();
-                if (!ok) why = "mk_rtc wrote no code";
-            } else if (ran) {
-                why = read_file(log, 480);
-            }
-        }
-        posix_spawn_file_actions_destroy(&fa);
-    }
-    (void)unlink(in.c_str());
-    (void)unlink(out.c_str());
-    (void)unlink(log.c_str());
-    (void)rmdir(dir.c_str());
-    return ran;
-}
-
-// Code object version of the native tier's modules, in process and in mk_rtc
-// alike: v5, which every HIP runtime a caller may bring understands.  ROCm
+// Code object version of the native tier's modules: v5, which every HIP runtime a caller may bring understands.  ROCm
 // 7.2's hiprtc defaults to v6; loaded into PyTorch's bundled (ROCm 7.0) HIP
 // runtime, v6 modules of the machine shape left the host heap corrupted at
 // process exit (free(): corrupted unsorted chunks after 60 dynamic-stack
@@ -2587,9 +2532,18 @@ constexpr const char *kCodeObjectVersion = "-mcode-object-version=5";
 // opened, and setenv (os.environ[...] = ... in Python) later reallocates and
 // frees that array: comgr's getenv then read freed memory (r04: SIGSEGV in
 // the compile thread after a test's monkeypatch.setenv).  Each compile gives
-// the namespace a private copy of the current environment instead; only the
-// compile thread touches it.
-void ns_environ_refresh(const RtcApi &rt)
+// the namespace a private copy of the environment instead: copied from
+// `environ` on the caller's thread when the compile is requested
+// (rtc_compile, so no compile thread walks the process's array while another
+// thread may setenv), installed by the compile thread, which alone reads it.
+std::vector<std::string> environ_snapshot()
+{
+    std::vector<std::string> s;
+    for (char **e = environ; e && *e; ++e) s.emplace_back(*e);
+    return s;
+}
+
+void ns_environ_install(const RtcApi &rt, const std::vector<std::string> &snapshot)
 {
     // one copy per namespace (its worker alone refreshes it): a refresh for
     // one namespace must not free the strings another's compile still reads
@@ -2606,8 +2560,7 @@ void ns_environ_refresh(const RtcApi &rt)
     }
     std::vector<std::string> &strings = env->strings;
     std::vector<char *> &ptrs = env->ptrs;
-    std::vector<std::string> s;
-    for (char **e = environ; e && *e; ++e) s.emplace_back(*e);
+    std::vector<std::string> s(snapshot);
     std::vector<char *> p;
     p.reserve(s.size() + 1);
     for (std::string &x : s) p.push_back(&x[0]);
@@ -2618,9 +2571,10 @@ void ns_environ_refresh(const RtcApi &rt)
 }
 
 // In-process hiprtc (the linked symbols, or this ROCm's namespace copy).
-void rtc_inproc(const RtcApi &rt, const std::string &src, bool &ok, std::string &why, std::vector<char> &code)
+void rtc_inproc(const RtcApi &rt, const HiprtcJob &j, bool &ok, std::string &why, std::vector<char> &code)
 {
-    if (rt.environ_ns) ns_environ_refresh(rt);
+    if (rt.environ_ns) ns_environ_install(rt, j.env);
+    const std::string &src = j.src;
     hiprtcProgram prog;
     if (rt.create(&prog, src.c_str(), "mk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         why = "hiprtcCreateProgram failed";
@@ -2651,6 +2605,28 @@ bool rtc_abandoned(HiprtcJob &j)
     return j.abandoned;
 }
 
+// The namespace compiler could not be opened (its reason, e.g. the dlmopen
+// error): modules then come from the linked hiprtc ("linked-other" in a
+// PyTorch process, whose code differs).  Said once on stderr
+// and kept for mk_net_plan (rtc_ns_error=).
+std::mutex g_ns_fail_mu;
+std::string g_ns_fail;
+
+void ns_degraded(const std::string &why)
+{
+    std::lock_guard<std::mutex> lk(g_ns_fail_mu);
+    if (!g_ns_fail.empty()) return;
+    g_ns_fail = why.empty() ? std::string("namespace compiler unavailable") : why;
+    fprintf(stderr, "mk: native-tier namespace compiler unavailable (%s); compiling with the linked hiprtc\n",
+            g_ns_fail.c_str());
+}
+
+std::string ns_fail_reason()
+{
+    std::lock_guard<std::mutex> lk(g_ns_fail_mu);
+    return g_ns_fail;
+}
+
 // One compile with the chosen compiler.  The linked hiprtc is the fallback
 // when the chosen one cannot run -- unless the caller has given up by then,
 // whose result nobody would read.
@@ -2662,18 +2638,19 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
     const RtcChoice ch = rtc_choice();
     bool ran = false;
     std::string from;
-    if (ch.kind == RTC_HELPER && !ch.helper.empty()) {
-        ran = rtc_spawn(ch.helper, *j, ok, why, code);
-        from = "helper";
+    if (ch.kind == RTC_REFUSED) {
+        ran = true; // nothing compiles: the network stays on tier 2
+        why = ch.why;
     } else if (ch.kind == RTC_NS || (ch.kind == RTC_LINKED && linked_stuck())) {
         NsCompiler &w = NsPool::get().pick();
         w.run(j, [&] {
             if (const RtcApi *rt = ns_rtc(w.index(), why)) {
-                rtc_inproc(*rt, j->src, ok, why, code);
+                rtc_inproc(*rt, *j, ok, why, code);
                 ran = true;
                 from = "ns";
             }
         });
+        if (!ran) ns_degraded(why);
     }
     if (!ran && !rtc_abandoned(*j)) {
         why.clear();
@@ -2684,7 +2661,7 @@ void hiprtc_run(const std::shared_ptr<HiprtcJob> &j)
                                    g_linked_running.end());
             g_linked_running.push_back(j);
         }
-        rtc_inproc(kLinkedRtc, j->src, ok, why, code);
+        rtc_inproc(kLinkedRtc, *j, ok, why, code);
         from = inproc_rtc_differs() ? "linked-other" : "linked";
     }
     if (ok) why = from; // which compiler's module (mk_net_plan)
@@ -2708,12 +2685,13 @@ uint64_t src_hash(const std::string &src)
     return h;
 }
 
-// One module through hiprtc_run on a helper thread, abandoned after max_s
+// One module through hiprtc_run on a compile thread, abandoned after max_s
 // seconds (`why` says so).  `from` = which compiler built it.
 bool rtc_compile(const std::string &src, double max_s, std::vector<char> &code, std::string &why, std::string &from)
 {
     auto job = std::make_shared<HiprtcJob>();
     job->src = src;
+    job->env = environ_snapshot(); // on the caller's thread (ns_environ_install)
     if (const char *d = std::getenv("MK_JIT_DUMP_SRC"); d && *d) { // diagnostics: every source, before it compiles
         char name[64];
         snprintf(name, sizeof name, "/%016llx.hip", (unsigned long long)src_hash(src));
@@ -2727,8 +2705,7 @@ bool rtc_compile(const std::string &src, double max_s, std::vector<char> &code, 
     std::unique_lock<std::mutex> lk(job->mu);
     const auto limit = std::chrono::duration<double>(max_s);
     if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
-        job->abandoned = true; // a helper child is killed; an in-process compile runs out
-        if (job->pid > 0) (void)kill(job->pid, SIGKILL);
+        job->abandoned = true; // the compile runs out in the background, its result discarded
         char b[128];
         snprintf(b, sizeof b, "hiprtc did not finish within the native tier's compile bound (%.0f s)", max_s);
         why = b;
@@ -3963,6 +3940,13 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                  sc->jit.src_bytes, (unsigned long long)sc->jit.src_hash,
                  sc->jit.code.size(), sc->jit.compile_s, sc->jit.rtc.c_str());
         s = std::string("tier=native ") + buf + tail;
+        if (sc->jit.rtc == "linked-other") { // the namespace compiler was wanted but could not open
+            std::string r = mk::ns_fail_reason();
+            if (!r.empty()) {
+                std::replace(r.begin(), r.end(), ' ', '_');
+                s += " rtc_ns_error=" + r;
+            }
+        }
         // heavy kernel, slots in HBM: at most this many inputs per launch
         // (the slot memory cap, JitLimits::slot_bytes; launch_jit_locked)
         const uint32_t hbm_slots = P.nslots - sc->jit.lds_n;

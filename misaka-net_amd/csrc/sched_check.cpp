@@ -526,4 +526,29 @@ int mkc_tier(void *hv, uint32_t cap, int soo, char *why, size_t why_len)
     return tier;
 }
 
+// The front end alone (tis_front.cpp parse_program), in mk_tokenize's output
+// form: token vectors, lines joined by '\n', tokens by '\x1f'; 0 or the
+// Go error text with -2 (MK_EPARSE); -3 when `out` is too small.  For the
+// sanitized build, which runs the front-end golden vectors through it.
+int mkc_tokenize(const char *program, char *out, size_t out_len)
+{
+    if (!program || !out || !out_len) return -1;
+    mk::Program P;
+    std::string err, s;
+    const bool ok = mk::parse_program(program, P, err);
+    if (!ok) {
+        s = err;
+    } else {
+        for (size_t i = 0; i < P.lines.size(); i++) {
+            if (i) s += '\n';
+            s += mk::form_name(P.lines[i].form);
+            if (!P.lines[i].a.empty()) { s += '\x1f'; s += P.lines[i].a; }
+            if (!P.lines[i].b.empty()) { s += '\x1f'; s += P.lines[i].b; }
+        }
+    }
+    if (s.size() + 1 > out_len) return -3;
+    std::memcpy(out, s.c_str(), s.size() + 1);
+    return ok ? 0 : -2;
+}
+
 } // extern "C"

@@ -76,3 +76,88 @@ def verify_gathered(g_out, g_st, full) -> bool:
 
     of, sf = full()
     return bool(torch.equal(of.to(g_out.device), g_out) and torch.equal(sf.to(g_st.device), g_st))
+
+
+# ---- self-launch: `python bench.py --gpus N` without torch.distributed.run --
+#
+# The driver's scaling command is a bare `python3 bench.py --gpus N`.  The
+# parent then starts N fresh child processes (one per GPU, the same argv, the
+# rendezvous variables torch.distributed.run would set) before it has loaded
+# the executor library or touched a GPU, and it never exec()s itself.  The
+# functions below use only the standard library, so a launching parent stays
+# GPU-free.
+
+LAUNCH_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+              "MASTER_ADDR", "MASTER_PORT")
+
+
+def needs_launch(gpus: int, environ) -> bool:
+    """True when N > 1 ranks were asked for and no launcher started this process."""
+    return gpus > 1 and "WORLD_SIZE" not in environ
+
+
+def free_port(addr: str = "127.0.0.1") -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind((addr, 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base, world: int, rank: int, port: int, addr: str = "127.0.0.1") -> dict:
+    """Environment of child `rank` of a single-node job of `world` ranks (the
+    variables torch.distributed.run exports; LOCAL_RANK selects the GPU)."""
+    env = {k: v for k, v in base.items() if k not in LAUNCH_ENV}
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", ROLE_RANK=str(rank), MASTER_ADDR=addr, MASTER_PORT=str(port))
+    return env
+
+
+def launch_ranks(argv, world: int, environ=None, port: int = 0, poll: float = 0.1, grace: float = 15.0,
+                 log=None) -> int:
+    """Run `argv` as `world` child processes, rank r with rank_env(r), and
+    wait for them.  Rank 0's stdout is the parent's (it prints the job's one
+    JSON line); the other ranks' stdout goes to the parent's stderr.  If a
+    rank fails, the others are terminated (their exact PIDs, SIGTERM then
+    SIGKILL after `grace` s) so none is left waiting in a collective.  Returns
+    0 when every rank exited 0, else the first failure's code (a signal as
+    128 + signo)."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    environ = os.environ if environ is None else environ
+    log = log or (lambda *a: print(*a, file=sys.stderr, flush=True))
+    port = port or free_port()
+    procs = []
+    rc = 0
+    try:
+        for r in range(world):
+            out = None if r == 0 else sys.stderr.fileno()
+            procs.append(subprocess.Popen(list(argv), env=rank_env(environ, world, r, port), stdout=out))
+        live = set(range(world))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    log(f"launch: rank {r} exited with {code}; stopping the other ranks")
+            if rc:
+                break
+            time.sleep(poll)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.monotonic() + grace
+        for p in procs:
+            try:
+                p.wait(max(0.0, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc

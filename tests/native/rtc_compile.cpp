@@ -1,15 +1,16 @@
-// mk_rtc.cpp -- the native tier's compiler process: compiles one generated
-// module (tis_jit.h jit_module_source) for gfx950 with this ROCm install's
-// hiprtc and writes the code object.
+// rtc_compile.cpp -- TEST TOOL (not part of the product): compiles one
+// generated module (tis_jit.h jit_module_source / the session module) for
+// gfx950 with this ROCm install's hiprtc, in a process of its own that never
+// loads PyTorch, and writes the code object.
 //
-//   mk_rtc SOURCE_FILE CODE_OBJECT_FILE
+//   rtc_compile SOURCE_FILE CODE_OBJECT_FILE
 //
-// mk_exec.hip runs it as a child process: in a process that imported
-// PyTorch first, PyTorch's bundled libhiprtc / libamd_comgr (the same
-// sonames, an older LLVM) are what the linked hiprtc symbols resolve to,
-// and they generate slower code (C4 D=256: 132 VGPRs and 325 us per launch
-// against 75 VGPRs and 195 us).  Exit status 0 = code written; otherwise the
-// compiler log is on stdout.
+// Tests use it (built by tests/schedcheck.py rtc_tool) to check that the
+// generated sources compile without a GPU, and that the executor's in-process
+// namespace compiler (mk_exec.hip ns_rtc) yields byte-identical code objects.
+// Until round 5 the product ran this as a child process of a GPU-initialised
+// process (MK_HIPRTC=helper); that path was removed.  Exit
+// status 0 = code written; otherwise the compiler log is on stdout.
 #include <hip/hiprtc.h>
 
 #include <cstdio>
@@ -21,7 +22,7 @@
 int main(int argc, char **argv)
 {
     if (argc != 3) {
-        std::printf("usage: mk_rtc SOURCE_FILE CODE_OBJECT_FILE\n");
+        std::printf("usage: rtc_compile SOURCE_FILE CODE_OBJECT_FILE\n");
         return 2;
     }
     std::ifstream in(argv[1], std::ios::binary);
@@ -29,7 +30,7 @@ int main(int argc, char **argv)
     ss << in.rdbuf();
     const std::string src = ss.str();
     if (src.empty()) {
-        std::printf("mk_rtc: empty source %s\n", argv[1]);
+        std::printf("rtc_compile: empty source %s\n", argv[1]);
         return 2;
     }
     hiprtcProgram prog;
@@ -58,7 +59,7 @@ int main(int argc, char **argv)
         std::ofstream out(argv[2], std::ios::binary);
         out.write(code.data(), (std::streamsize)code.size());
         if (!out) {
-            std::printf("mk_rtc: cannot write %s\n", argv[2]);
+            std::printf("rtc_compile: cannot write %s\n", argv[2]);
             rc = 1;
         }
     }

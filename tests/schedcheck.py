@@ -10,6 +10,9 @@ import misaka_net_amd as mk
 from misaka_net_amd import _native as N
 
 LIB = os.path.join(os.path.dirname(mk._native.LIB_PATH), "libmisaka_amd_check.so")
+# MK_CHECK_LIB: another build of the same sources (the ASan + UBSan one,
+# __graft_entry__.build_check(sanitize=True), tests/test_sanitized.py)
+SAN = os.environ.get("MK_CHECK_LIB")
 _lib = None
 
 
@@ -18,8 +21,11 @@ def lib():
     if _lib is None:
         import __graft_entry__ as g
 
-        g.build_check()
-        h = C.CDLL(LIB)
+        if SAN:
+            assert os.path.exists(SAN), SAN
+        else:
+            g.build_check()
+        h = C.CDLL(SAN or LIB)
         h.mkc_load.restype = C.c_void_p
         h.mkc_load.argtypes = [C.POINTER(N.mk_node_desc), C.c_int, C.c_char_p, C.c_size_t]
         h.mkc_free.argtypes = [C.c_void_p]
@@ -28,12 +34,25 @@ def lib():
         h.mkc_jit_lane.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         h.mkc_tier.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_char_p, C.c_size_t]
+        h.mkc_tokenize.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
         _lib = h
     return _lib
 
 
 class NotCompiled(Exception):
     pass
+
+
+def tokenize(program: str):
+    """The check library's front end (sched_check.cpp mkc_tokenize): the
+    token vectors of misaka_net_amd.tokenize, or TisParseError."""
+    buf = C.create_string_buffer(max(4096, 64 * len(program) + 1024))
+    rc = lib().mkc_tokenize(program.encode(), buf, len(buf))
+    text = buf.value.decode(errors="surrogateescape")
+    if rc == -2:
+        raise mk.TisParseError(text)
+    assert rc == 0, rc
+    return [line.split("\x1f") for line in text.split("\n")]
 
 
 def _load(nodes):
@@ -220,3 +239,35 @@ def session_module(nodes, *, stack_cap=None):
         return buf.value.decode()
     finally:
         lib().mkc_free(h)
+
+
+# ---- test tool: a standalone hiprtc compiler (tests/native/rtc_compile.cpp)
+
+_TOOL_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+
+
+def rtc_tool():
+    """Path of the built test compiler (this ROCm's hiprtc in a process of its
+    own that never loads PyTorch); rebuilt when its source changes."""
+    import hashlib
+    import subprocess
+
+    src = os.path.join(_TOOL_DIR, "rtc_compile.cpp")
+    out = os.path.join(_TOOL_DIR, "build", "rtc_compile")
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", src,
+           "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
+    with open(src, "rb") as f:
+        stamp = hashlib.sha256(f.read() + " ".join(cmd).encode()).hexdigest()
+    try:
+        with open(out + ".stamp") as f:
+            if f.read().strip() == stamp and os.path.exists(out):
+                return out
+    except OSError:
+        pass
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = f"{out}.tmp{os.getpid()}"
+    subprocess.check_call(cmd + ["-o", tmp])
+    os.replace(tmp, out)
+    with open(out + ".stamp", "w") as f:
+        f.write(stamp + "\n")
+    return out

@@ -95,6 +95,87 @@ def test_two_rank_shard_reduce_gather():
 _port_holder = [_port()]
 
 
+def test_rank_env_construction():
+    # the variables torch.distributed.run exports, one set per child; stale
+    # launcher variables in the parent's environment never leak through
+    base = {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0", "RANK": "5", "MASTER_PORT": "1"}
+    envs = [mk.dist.rank_env(base, 4, r, 29511) for r in range(4)]
+    for r, e in enumerate(envs):
+        assert e["RANK"] == e["LOCAL_RANK"] == e["ROLE_RANK"] == str(r)
+        assert e["WORLD_SIZE"] == e["LOCAL_WORLD_SIZE"] == "4" and e["GROUP_RANK"] == "0"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29511"
+        assert e["PATH"] == "/usr/bin" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert base["RANK"] == "5"  # the parent's mapping is not modified
+    assert mk.dist.needs_launch(8, {}) and not mk.dist.needs_launch(1, {})
+    assert not mk.dist.needs_launch(8, {"WORLD_SIZE": "8"})  # already under a launcher
+
+
+def test_bench_self_launch_argv(monkeypatch):
+    # bench.py's parent: --gpus N read before anything touches a GPU, the
+    # children get the same argv (so each parses --gpus N and WORLD_SIZE=N)
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    assert bench._gpus_arg(["--gpus", "8", "--steps", "20", "--warmup", "3"]) == 8
+    assert bench._gpus_arg(["--steps", "5"]) == 1
+    seen = {}
+
+    def fake_launch(argv, world, **kw):
+        seen.update(argv=argv, world=world)
+        return 0
+
+    monkeypatch.setattr(mk.dist, "launch_ranks", fake_launch)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    import runpy
+
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "7"])
+    try:
+        runpy.run_path(bench.__file__, run_name="__main__")
+    except SystemExit as e:
+        assert e.code == 0
+    assert seen["world"] == 4 and seen["argv"][1:] == [os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "7"]
+
+
+_CHILD = r"""
+import json, os, sys, time
+r = int(os.environ["RANK"])
+with open(os.path.join(sys.argv[1], f"rank{r}.json"), "w") as f:
+    json.dump({k: os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}, f)
+mode = sys.argv[2]
+if mode == "fail" and r == 1:
+    sys.exit(3)
+if mode == "fail":
+    time.sleep(120)  # would hang the job if the launcher did not stop it
+print(json.dumps({"rank": r}) if r == 0 else "not-on-stdout", flush=True)
+"""
+
+
+def test_launch_ranks_children(tmp_path, capfd):
+    import sys
+
+    rc = mk.dist.launch_ranks([sys.executable, "-c", _CHILD, str(tmp_path), "ok"], 3)
+    assert rc == 0
+    import json
+
+    envs = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] and {e["WORLD_SIZE"] for e in envs} == {"3"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+    out, err = capfd.readouterr()
+    assert out.strip().splitlines() == ['{"rank": 0}']  # only rank 0 on stdout
+    assert err.count("not-on-stdout") == 2
+
+
+def test_launch_ranks_failure_stops_the_others(tmp_path):
+    import sys
+    import time
+
+    t0 = time.monotonic()
+    rc = mk.dist.launch_ranks([sys.executable, "-c", _CHILD, str(tmp_path), "fail"], 2, grace=5.0)
+    assert rc == 3 and time.monotonic() - t0 < 60
+
+
 def test_split_covers_batch():
     for total in (0, 1, 7, 64, 1000003):
         for world in (1, 2, 3, 8):

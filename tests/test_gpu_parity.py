@@ -413,6 +413,28 @@ def test_c3_64m_shard_properties(gpu, mode):
             assert (sp[cls] == oracle(nodes, x[i:i + 1])[2][0]).all()
 
 
+@pytest.mark.parametrize("mode", ["auto", "interp"])
+def test_c3_full_64m_equals_eight_shards(gpu, mode):
+    # BASELINE config 3 end to end: one launch over all 67,108,864 global
+    # lanes equals the concatenation of the 8 rank shards (8,388,608 lanes at
+    # offsets r * 8,388,608, inputs generated from the global lane index) --
+    # the order bench.py's RCCL gather to rank 0 must reproduce
+    # (misaka_net_amd.dist.shard / timed_gather).  out, status and steps
+    # bit-exact; the retired-instruction counters add up.
+    shard, world = 1 << 23, 8
+    net = mk.Network(mk.networks.sample_network())
+    full = _device_run(net, world * shard, offset=0, mode=_m(mode))
+    tot = np.zeros(N.MK_STATS_LEN, np.int64)
+    for r in range(world):
+        lo, hi = mk.dist.shard(r, shard)
+        part = _device_run(net, shard, offset=lo, mode=_m(mode))
+        for a, b, what in zip(full[:3], part[:3], ("out", "status", "steps")):
+            bad = np.nonzero(a[lo:hi] != b)[0]
+            assert not bad.size, f"rank {r} shard: {what} differs at global lane {lo + int(bad[0])}"
+        tot += part[3]
+    assert tot[0] == full[3][0] and tot[1] == full[3][1] and tot[2] == full[3][2] == world * shard
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_c5_full_size_properties(gpu, mode):
     # the C5 bench workload: 4,194,304 lanes, masked inputs 0..1023.  The

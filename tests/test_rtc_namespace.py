@@ -54,8 +54,12 @@ def test_plain_process_uses_linked_hiprtc():
     assert "('linked', 6)" in line, line
 
 
-def test_namespace_and_helper_modules_are_identical(tmp_path):
-    # the namespace copy is the helper's compiler: byte-identical code objects
+def test_namespace_and_standalone_modules_are_identical(tmp_path):
+    # the namespace copy is this ROCm's compiler: its code object is
+    # byte-identical to the standalone test compiler's (a process that never
+    # loads PyTorch) for the same generated source
+    import schedcheck as sc
+
     code = r"""
 import os, sys
 sys.path[:0] = [{root!r}]
@@ -63,17 +67,37 @@ import torch  # noqa: F401
 import misaka_net_amd as mk
 print(mk.Network(mk.networks.pipeline_network(256)).plan().split("rtc=")[1].split()[0])
 """
-    out = {}
-    for mode in ("ns", "helper"):
-        dump = str(tmp_path / f"{mode}.co")
-        e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_DUMP=dump)
-        r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True,
-                           timeout=600, env=e)
-        assert r.returncode == 0, r.stderr[-2000:]
-        assert r.stdout.split()[-1] == mode
-        with open(dump, "rb") as f:
-            out[mode] = f.read()
-    assert out["ns"] and out["ns"] == out["helper"]
+    dump = str(tmp_path / "ns.co")
+    e = dict(os.environ, MK_HIPRTC="ns", MK_JIT_DUMP=dump)
+    r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=600, env=e)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-1] == "ns"
+    alone = str(tmp_path / "alone.co")
+    t = subprocess.run([sc.rtc_tool(), dump + ".hip", alone], capture_output=True, text=True, timeout=600)
+    assert t.returncode == 0, t.stdout[-2000:]
+    with open(dump, "rb") as f, open(alone, "rb") as g:
+        a, b = f.read(), g.read()
+    assert a and a == b
+
+
+@pytest.mark.parametrize("mode", ["helper", "/usr/bin/true"])
+def test_helper_process_compiler_is_refused(mode):
+    # the round-3 helper child process (posix_spawn from a compile thread of
+    # a GPU-initialised process, DESIGN.md 4b) no longer exists: asking for
+    # it keeps the network off the native tier, with the reason in the plan
+    code = r"""
+import os, sys
+sys.path[:0] = [{root!r}]
+import misaka_net_amd as mk
+print("RESULT", mk.Network(mk.networks.example_network()).plan())
+"""
+    e = dict(os.environ, MK_HIPRTC=mode)
+    r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True, timeout=600,
+                       env=e)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plan = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1]
+    assert "tier=compiled" in plan and "MK_HIPRTC" in plan and "rtc=" not in plan, plan
 
 
 @pytest.mark.parametrize("torch_first", [True])

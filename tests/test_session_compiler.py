@@ -234,12 +234,12 @@ def test_generated_session_lane(tmp_path):
 
 def test_session_modules_compile_for_gfx950(tmp_path):
     # the whole module (lane + mk_sess_exec) through this ROCm's hiprtc, as
-    # the loader compiles it (mk_rtc; no GPU needed)
+    # the loader compiles it (the standalone test compiler; no GPU needed)
     import subprocess
 
     import schedcheck as sc
 
-    rtc = os.path.join(os.path.dirname(mk._native.LIB_PATH), "mk_rtc")
+    rtc = sc.rtc_tool()
     for name, nodes in [("example", mk.networks.example_network()), ("countdown", mk.networks.countdown_network()),
                         ("pipeline64", mk.networks.pipeline_network(64)), ("rand3", random_network(3))]:
         src = sc.session_module(nodes)

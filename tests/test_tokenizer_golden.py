@@ -29,6 +29,15 @@ def test_product_parser_matches_reference_regexes():
     assert not bad, bad[:3]
 
 
+def test_check_library_front_end_matches_reference_regexes():
+    # the same parser built into the CPU check library (and, under
+    # tests/test_sanitized.py, its ASan + UBSan build)
+    import schedcheck as sc
+
+    bad = [(p, r, got) for p, r in VECS if (got := _run(sc.tokenize, mk.TisParseError, p)) != r]
+    assert not bad, bad[:3]
+
+
 def test_oracle_matches_reference_regexes():
     bad = [(p, r, got) for p, r in VECS if (got := _run(po.tokenize, po.OracleParseError, p)) != r]
     assert not bad, bad[:3]
