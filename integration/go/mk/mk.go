@@ -16,6 +16,7 @@ import "C"
 import (
 	"fmt"
 	"sort"
+	"strings"
 	"unsafe"
 )
 
@@ -92,6 +93,27 @@ func Load(nodes []Node) (*Net, error) {
 		return nil, fmt.Errorf("%s", C.GoString((*C.char)(unsafe.Pointer(&errBuf[0]))))
 	}
 	return &Net{h: h}, nil
+}
+
+// Tokenize is tis.Tokenize (tokenizer.go:29-106) on one program: its token
+// vectors, or the reference's error text (mk_tokenize).
+func Tokenize(program string) ([][]string, error) {
+	cs := C.CString(program)
+	defer C.free(unsafe.Pointer(cs))
+	buf := make([]byte, 64*len(program)+4096)
+	rc := C.mk_tokenize(cs, (*C.char)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)))
+	text := C.GoString((*C.char)(unsafe.Pointer(&buf[0])))
+	if rc == C.MK_EPARSE {
+		return nil, fmt.Errorf("%s", text)
+	}
+	if rc != C.MK_OK {
+		return nil, fmt.Errorf("mk_tokenize: %d", int(rc))
+	}
+	var out [][]string
+	for _, line := range strings.Split(text, "\n") {
+		out = append(out, strings.Split(line, "\x1f"))
+	}
+	return out, nil
 }
 
 // Close frees the network (after every Sessions of it is closed).

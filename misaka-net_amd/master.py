@@ -20,9 +20,12 @@ Deliberate differences (DESIGN.md / INTEGRATION.md):
   * by default (``stateful=True``) the reference's semantics: one network
     instance whose node state, stacks and channels persist across /compute
     calls (program.go:80-92, master.go:216-219), on the GPU (SessionSet, row
-    f2); /reset and /load reset it, /pause keeps it.  Concurrent /compute
-    requests are coalesced: the ones that arrive while a launch is in flight
-    run, in arrival order, as sequential calls of the next single launch
+    f2); /reset and /load reset it, /pause keeps it (a call in flight when
+    /pause comes stays open and waits, as the reference's handler stays
+    blocked on outChan while the nodes are paused; /run lets it continue,
+    its ``call_timeout`` still running; /reset and /load end it, 504).
+    Concurrent /compute requests are coalesced: the ones that arrive while a
+    launch is in flight run, in arrival order, as sequential calls of the next single launch
     (mk_session_compute_seq) -- the reference serves them one at a time
     through its capacity-1 inChan/outChan.
   * ``stateful=False`` is the batch extension (the lane model): every input
@@ -187,7 +190,8 @@ class MasterNode:
         self._lock = threading.Lock()
         self._burst = threading.Lock()
         self._exec = threading.Lock()
-        self._epoch = 0
+        self._epoch = 0  # bumped by /reset and /load (under _exec): calls in flight end
+        self._running = threading.Event()  # is_running, for calls waiting out a /pause
         # cmd/app.go:21-24: a PROGRAM that fails to load is logged and the node
         # keeps its default program ([["NOP"]], program.go:64)
         for k, text in (programs or {}).items():
@@ -266,6 +270,8 @@ class MasterNode:
         with self._burst:
             epoch = self._epoch
             while len(res) < len(vals):
+                if not self._wait_running(epoch, deadline):
+                    break
                 with self._exec:
                     if self._epoch != epoch:
                         break
@@ -288,12 +294,31 @@ class MasterNode:
         res += [(False, 0, N.MK_ST_BUDGET)] * (len(vals) - len(res))
         return res
 
+    def _wait_running(self, epoch, deadline) -> bool:
+        """Wait out a /pause: the nodes do not run, and the reference's
+        handler stays blocked on outChan until /run (master.go:216-219,
+        program.go:80-92).  False when /reset or /load ended the burst, or
+        its deadline passed."""
+        while not self._running.is_set():
+            if self._epoch != epoch:
+                return False
+            wait = 0.02
+            if deadline is not None:
+                wait = min(wait, deadline - time.monotonic())
+                if wait <= 0:
+                    return False
+            self._running.wait(wait)
+        return self._epoch == epoch
+
     def _finish_open_call(self, sess, epoch, deadline):
         while True:
-            with self._exec:
-                if self._epoch != epoch or self._sess is not sess:
-                    if self._sess is sess:  # /pause: the instance stays, its open call goes
+            if not self._wait_running(epoch, deadline):
+                with self._exec:
+                    if self._sess is sess and self._epoch == epoch:  # the deadline passed while paused
                         sess.cancel()
+                return False, 0, N.MK_ST_BUDGET
+            with self._exec:
+                if self._epoch != epoch or self._sess is not sess:  # /reset or /load
                     return False, 0, N.MK_ST_BUDGET
                 r = sess.resume(steps=False)
                 o, st = int(r.out[0]), int(r.status[0])
@@ -342,6 +367,7 @@ class MasterNode:
     def _run(self, *_):
         with self._lock:
             self.is_running = True  # master.go:93 sets it before broadcasting
+            self._running.set()
             e = self._check_types()
             if e:
                 return http_error(f"error running network: {e}", 400)
@@ -353,7 +379,7 @@ class MasterNode:
             if e:
                 return http_error(f"error pausing network: {e}", 400)
             self.is_running = False
-            self._epoch += 1  # a call being resumed stops at its next slice (cancelled)
+            self._running.clear()  # a call in flight waits at its next slice, open, until /run
             if self.wire is not None:
                 self.wire.cancel()  # stopNode: blocked GetInput calls return errors (master.go:117-119, 251-260)
             return Response(200, "Success")
@@ -364,8 +390,9 @@ class MasterNode:
             if e:
                 return http_error(f"error resetting network: {e}", 400)
             self.is_running = False
-            self._epoch += 1
+            self._running.clear()
             with self._exec:  # at most one launch in flight to wait for
+                self._epoch += 1  # a call in flight ends at its next slice
                 # resetNode on every node and the master's channels (master.go:129-138)
                 self._drop_state(keep_session=True)
             if self.wire is not None:
@@ -386,26 +413,37 @@ class MasterNode:
             e = self._check_types()
             if e:
                 return http_error(f"error resetting network: {e}", 400)
+            # ProgramNode.LoadProgram's parse (program.go:178-193) first: it
+            # changes nothing
+            err = None
+            if self.node_info[target].get("type") != "program":
+                err = "not a program node"
+            else:
+                try:
+                    tokenize(program)
+                except TisParseError as ex:
+                    err = str(ex)
             # /load resets the whole network before the Load RPC, whatever the
             # RPC then does (master.go:165-175: broadcast reset, stopNode,
-            # resetNode): node state, stacks and the master's channels
+            # resetNode): node state, stacks and the master's channels.  All
+            # of it in one executor section: a burst between two
+            # sections would build a session on the old network, which the
+            # second section then freed under it.  After this section the
+            # next network() / session() is built from the new program.
             self.is_running = False
-            self._epoch += 1
+            self._running.clear()
             with self._exec:
+                self._epoch += 1
                 self._drop_state()
+                if err is None:
+                    self.programs[target] = program
+                    if self._net is not None:
+                        self._net.close()
+                        self._net = None
             if self.wire is not None:
                 self.wire.reset()
-            if self.node_info[target].get("type") != "program":
-                return http_error(f"error loading program on node {target}: not a program node", 400)
-            try:
-                tokenize(program)  # ProgramNode.LoadProgram's parse (program.go:178-193)
-            except TisParseError as ex:
-                return http_error(f"error loading program on node {target}: {ex}", 400)
-            self.programs[target] = program
-            with self._exec:
-                if self._net is not None:
-                    self._net.close()
-                    self._net = None
+            if err is not None:
+                return http_error(f"error loading program on node {target}: {err}", 400)
             return Response(200, "Success")
 
     def _values(self, form, key="value"):

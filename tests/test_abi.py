@@ -60,7 +60,32 @@ def test_go_adapter_binds_only_declared_symbols():
     used = set(re.findall(r"\bC\.(mk_[a-z_0-9]+)\b", src))
     types = {"mk_net", "mk_session", "mk_opts", "mk_node_desc", "mk_remote_req", "mk_trace_entry"}
     assert used - types <= set(declared_functions()), used - types - set(declared_functions())
-    assert {"mk_net_load", "mk_compute_batch", "mk_session_create", "mk_session_compute"} <= used
+    assert {"mk_net_load", "mk_compute_batch", "mk_session_create", "mk_session_compute", "mk_tokenize"} <= used
+
+
+def test_go_master_adapter_routes_and_locking():
+    # integration/go/gpumaster.go.txt (row f3, source only): every route of
+    # master.go:90-224 plus /compute_batch; isRunning only under g.mu (the
+    # reference reads and writes it unsynchronised, master.go:93,200)
+    src = open(os.path.join(ROOT, "integration", "go", "gpumaster.go.txt")).read()
+    routes = re.findall(r'post\("(/[a-z_]+)"', src)
+    assert sorted(routes) == sorted(["/run", "/pause", "/reset", "/load", "/compute", "/compute_batch"]), routes
+    for text in ("error loading program on node %s: %s", "node %s not valid on this network",
+                 "network is not running", "cannot parse form", "cannot parse value", "method GET not allowed",
+                 "error resetting network: %s"):
+        assert text in src, text
+    # every isRunning access sits in a region holding g.mu: within a function,
+    # after a g.mu.Lock() with no g.mu.Unlock() since, or in a function whose
+    # comment says the caller holds it
+    funcs = re.split(r"\n(?=func |\tpost\()", src)
+    for f in funcs:
+        for m in re.finditer(r"g\.isRunning", f):
+            before = f[:m.start()].replace("defer g.mu.Unlock()", "")
+            held = before.rfind("g.mu.Lock()") > before.rfind("g.mu.Unlock()") or "g.mu held" in f
+            assert held, f[:200]
+    # /load resets under the lock before it reloads: both in the one handler
+    load = src[src.index('post("/load"'):src.index('post("/compute"')]
+    assert load.index("g.mu.Lock()") < load.index("g.sess.Reset()") < load.index("g.build()")
 
 
 def _build_c_client(tmp_path):

@@ -9,6 +9,7 @@ import time
 import pytest
 
 import misaka_net_amd as mk
+from misaka_net_amd import _native as N
 from misaka_net_amd.master import Coalescer, MasterNode, go_atoi, make_server, parse_query
 
 NODE_INFO = {"misaka1": {"type": "program"}, "misaka2": {"type": "program"}, "misaka3": {"type": "stack"}}
@@ -428,17 +429,153 @@ def test_reset_during_a_spinning_call_returns_at_once():
     assert m._run_batch([7]) == [(True, 7)]
 
 
-def test_pause_during_a_spinning_call_cancels_it_and_keeps_state():
-    m = _stateful(SPINNER, sess_budget=1000, call_timeout=None)
+class _GateSession:
+    """A call that stays open (MK_ST_BUDGET each slice) until `gate` is set,
+    then answers 42: the master's resume loop without an executor."""
+
+    def __init__(self):
+        self.gate, self.launches, self.cancels = threading.Event(), 0, 0
+
+    def _res(self, o, st):
+        from misaka_net_amd.network import BatchResult
+        import numpy as np
+
+        return BatchResult(np.array([o], np.int32), np.array([st], np.uint8), None)
+
+    def compute_seq(self, vals, steps=False, busy_ok=False):
+        self.launches += 1
+        return self._res(0, N.MK_ST_BUDGET)
+
+    def resume(self, steps=False):
+        self.launches += 1
+        return self._res(42, N.MK_ST_HAS_OUTPUT | N.MK_ST_QUIESCENT) if self.gate.is_set() else \
+            self._res(0, N.MK_ST_BUDGET)
+
+    def cancel(self):
+        self.cancels += 1
+
+    def reset(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def test_pause_keeps_a_call_open_until_run():
+    # the reference's /compute handler stays blocked on outChan while the
+    # nodes are paused and answers once /run resumes them (master.go:216-219,
+    # program.go:80-92): no slice runs while paused, the call is not cancelled
+    m = _stateful(SPINNER, call_timeout=None)
+    g = m._sess = _GateSession()
     t, box = _spin_in_thread(m, 0)
     t0 = time.monotonic()
     assert m.handle("POST", "/pause").code == 200
     assert time.monotonic() - t0 < 0.5
-    t.join(timeout=5)
-    assert box["r"] == (504, "network produced no output\n")
+    time.sleep(0.1)
+    n = g.launches
+    time.sleep(0.3)
+    assert g.launches == n and t.is_alive() and g.cancels == 0  # waiting, open
+    assert _compute(m, 5) == (400, "network is not running\n")  # new calls: master.go:200-202
+    g.gate.set()
     m.handle("POST", "/run")
-    assert _compute(m, 5) == (200, '{"value":5}\n')  # the instance kept its state
-    assert getattr(m._sess, "resets", 0) == 0
+    t.join(timeout=5)
+    assert box["r"] == (200, '{"value":42}\n')
+
+
+def test_pause_then_reset_ends_the_open_call():
+    m = _stateful(SPINNER, call_timeout=None)
+    m._sess = _GateSession()
+    t, box = _spin_in_thread(m, 0)
+    m.handle("POST", "/pause")
+    time.sleep(0.1)
+    assert t.is_alive()
+    assert m.handle("POST", "/reset").code == 200
+    t.join(timeout=5)
+    assert not t.is_alive() and box["r"] == (504, "network produced no output\n")
+
+
+def test_call_timeout_runs_while_paused():
+    m = _stateful(SPINNER, call_timeout=0.3)
+    g = m._sess = _GateSession()
+    t, box = _spin_in_thread(m, 0)
+    m.handle("POST", "/pause")
+    t.join(timeout=5)
+    assert box["r"] == (504, "network produced no output\n") and g.cancels == 1
+
+
+class _FakeNet:
+    """Network stand-in for the /load race: a session built on a
+    closed network, or used after its network closed, is the use-after-free
+    the native handles would suffer."""
+    errors: list = []
+
+    def __init__(self, specs):
+        self.tag = {s.name: s.program for s in specs}.get("p", "")
+        self.closed = False
+
+    def sessions(self, n, **kw):
+        if self.closed:
+            _FakeNet.errors.append("session built on a closed network")
+        return _FakeSess(self)
+
+    def close(self):
+        self.closed = True
+
+
+class _FakeSess:
+    def __init__(self, net):
+        self.net, self.live = net, True
+
+    def compute_seq(self, vals, steps=False, busy_ok=False):
+        from misaka_net_amd.network import BatchResult
+        import numpy as np
+
+        if self.net.closed or not self.live:
+            _FakeNet.errors.append("session used after its network closed")
+        time.sleep(0.0005)  # a launch
+        v = int(self.net.tag.split()[1])  # "OUT <k>"
+        return BatchResult(np.full(len(vals), v, np.int32),
+                           np.full(len(vals), N.MK_ST_HAS_OUTPUT | N.MK_ST_QUIESCENT, np.uint8), None)
+
+    def reset(self):
+        pass
+
+    def close(self):
+        self.live = False
+
+
+def test_load_during_stateful_bursts_never_uses_the_old_network(monkeypatch):
+    # /compute bursts from 8 threads while /load replaces the program 40
+    # times: no session is built on, or runs after, a network that /load
+    # closed; once /load (+ /run) returned, every call answers the new program
+    from misaka_net_amd import master as M
+
+    monkeypatch.setattr(M, "Network", _FakeNet)
+    _FakeNet.errors = []
+    m = MasterNode({"p": {"type": "program"}}, {"p": "OUT 0"})
+    m.handle("POST", "/run")
+    stop = threading.Event()
+    seen = []
+
+    def client():
+        while not stop.is_set():
+            r = m.handle("POST", "/compute", body=b"value=1", ctype=FORM)
+            if r.code == 200:
+                seen.append(json.loads(r.body)["value"])
+
+    ts = [threading.Thread(target=client, daemon=True) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for k in range(1, 41):
+        assert m.handle("POST", "/load", body=f"program=OUT+{k}&targetURI=p".encode(), ctype=FORM).code == 200
+        m.handle("POST", "/run")
+        r = m.handle("POST", "/compute", body=b"value=1", ctype=FORM)
+        assert r.code == 200 and json.loads(r.body)["value"] == k, (k, r.body)
+    stop.set()
+    for t in ts:
+        t.join(10)
+    assert not _FakeNet.errors, _FakeNet.errors[:3]
+    assert len(seen) > 40
 
 
 def test_one_deadline_for_the_whole_burst():
@@ -483,6 +620,33 @@ def test_http_c3_zero_then_five(gpu):
         assert post(port, "/compute", "value=-3")[::2] == (200, '{"value":-6}\n')
     finally:
         srv.shutdown()
+
+
+@pytest.mark.gpu
+def test_gpu_load_during_concurrent_compute(gpu):
+    # ADVICE r04 on the executor: /compute from 4 threads while /load swaps
+    # the program 6 times; after each /load + /run the new program answers
+    m = MasterNode({"p": {"type": "program"}}, {"p": "IN ACC\nADD 0\nOUT ACC"})
+    m.handle("POST", "/run")
+    stop = threading.Event()
+    codes = []
+
+    def client():
+        while not stop.is_set():
+            codes.append(m.handle("POST", "/compute", body=b"value=1", ctype=FORM).code)
+
+    ts = [threading.Thread(target=client, daemon=True) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for k in range(1, 7):
+        assert m.handle("POST", "/load", body=f"program=IN+ACC%0AADD+{k}%0AOUT+ACC&targetURI=p".encode(),
+                        ctype=FORM).code == 200
+        m.handle("POST", "/run")
+        assert _compute(m, 1) == (200, f'{{"value":{1 + k}}}\n')
+    stop.set()
+    for t in ts:
+        t.join(30)
+    assert set(codes) <= {200, 400, 504} and codes.count(200) > 0
 
 
 @pytest.mark.gpu

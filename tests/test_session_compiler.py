@@ -16,6 +16,7 @@ import pytest
 import misaka_net_amd as mk
 from oracle import pyoracle as po
 import schedcheck as sc
+from misaka_net_amd import _native as N
 from schedcheck import HANDOFF, HostSessions, NotCompiled
 from tisgen import random_network, stack_loop_network
 
@@ -274,6 +275,16 @@ def test_session_call_bound_covers_every_call():
         for call in range(6):
             _, _, sp = emu.call(po.gen_inputs(0x4D49534B41 + call, 64))
             assert int(sp.max()) <= bound, (name, call, int(sp.max()), bound)
+        # the condition the one-launch shortcut relies on (mk_exec.hip session
+        # launch: call_steps < budget): at budget = bound + 1 neither the
+        # budget guard nor a round end fires, so no call hands off to the
+        # interpreter or stops on the budget
+        tight = sc.HostSessions(nodes, 64)
+        for call in range(6):
+            _, st, sp = tight.call(po.gen_inputs(0x4D49534B41 + call, 64), budget=bound + 1)
+            assert not (st == sc.HANDOFF).any(), (name, call, "handed off below the bound")
+            assert not ((st & N.MK_ST_REASON_MASK) == N.MK_ST_BUDGET).any(), (name, call, "budget stop")
+            assert int(sp.max()) <= bound
     assert seen_bounded >= 3
     assert sc.session_max_call_steps(mk.networks.countdown_network()) is None
     assert sc.session_max_call_steps(mk.networks.example_network()) is not None
