@@ -715,6 +715,18 @@ def main():
     # stacks kept there.
     bounds = [b for b in (hbm, issue, lds) if b and b.get("frac") is not None]
     headline = max(bounds, key=lambda b: b["frac"])
+    # What the node-instr/s figure is a count of: the
+    # executed VALU lane-ops per retired node-instruction from the matching
+    # PMC profile.  Well below 1, the compiler folded the program (C2, C3:
+    # two adds per lane; C4 d64: pushes forwarded to pops in registers) and
+    # node-instr/s counts the reference's work, not issued work: the bound
+    # is then the byte stream, reported as `roofline`.
+    vpi = prof.get("valu_lane_ops_per_instr") if sq.get("SQ_INSTS_VALU") else None
+    executed = {"valu_lane_ops_per_node_instr": vpi,
+                "compile_folded": None if vpi is None else bool(vpi < 1.0 and headline["bound"] != "valu"),
+                "bound": headline["bound"],
+                "note": "node-instr/s counts retired reference instructions; executed VALU lane-ops per "
+                        "node-instruction from the PMC profile of this module (null: no matching profile)"}
 
     http = None
     if args.http and rank == 0:
@@ -754,6 +766,7 @@ def main():
             "kernel_ms_per_step": kern_max / args.steps * 1e3,
             "host_enqueue_us_per_step": enqueue_s / args.steps * 1e6,
             "launch": "hip graph replay" if args.graph else "stream launches",
+            "executed": executed,
             "roofline": headline,
             "roofline_issue": issue,
             "roofline_hbm": hbm,

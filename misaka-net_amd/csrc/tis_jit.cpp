@@ -471,173 +471,6 @@ struct OpWriter {
     }
 };
 
-// Closed form of a pop run's register chain (round 4, MK_JIT_LIN_SUM=1, off
-// by default: measured neutral, see JitLimits::lin_sum).  When
-// every op of the period is linear -- LD, LI, MOV, ADD, SUB, ADDI, RSUBI --
-// the registers after j periods are an affine function of their values
-// before them and of the j periods' popped values: r' = sum c_s r_s +
-// sum d_i x_i + c.  C4's pop loop is `sum = 3 * sum + v`, one dependent
-// v_mad_u64_u32 (10.7 cycles at one wave per SIMD) per pop.  (The same
-// network with `sum = sum + v` ran 21.5 against 163.9 us at D = 256,
-// profiles/r04v_chain*.txt -- but there LLVM forwarded the LDS pushes to the
-// pops and summed the pushed sequence itself, so that was no measure of the
-// chain.)  A prefetched block of U periods runs its
-// first U - 1 in closed form -- the popped values combined by a balanced
-// tree (depth log2 of the pops; for C4's geometric weights 3^k each node is
-// one multiply-add, as many as the chain had), one multiply-add per carried
-// register -- and its last period as written.  Integer arithmetic is a ring
-// (mod 2^32 when every register the period writes is narrow, which also
-// makes the sext32 of a hop the identity; else mod 2^64 without truncating
-// operands), so the registers are bit-identical to running the chain.
-struct LinForm {
-    std::vector<uint64_t> reg, ld; // coefficients of the registers before the block, of its popped values
-    uint64_t c = 0;
-};
-
-struct LinSummary {
-    bool ok = false, mod32 = false;
-    std::vector<uint32_t> carried; // registers read before written in the period and written in it
-    std::vector<LinForm> F;        // their values after U - 1 periods
-};
-
-LinSummary lin_summary(const Graph &g, const Run &r, size_t nlds, size_t U)
-{
-    LinSummary S;
-    const size_t NR = g.used_reg.size(), NL = (U - 1) * nlds;
-    std::vector<char> wr(NR, 0), rd(NR, 0), narrow_ok(NR, 0);
-    bool trunc = false;
-    auto read = [&](uint32_t off) {
-        if (!wr[off / 8]) rd[off / 8] = 1;
-    };
-    for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
-        const DOp &I = g.D[pc];
-        switch (I.op) {
-        case U_LD: case U_LI: break;
-        case U_MOV: case U_ADDI: case U_RSUBI: read(I.a); trunc = trunc || (I.fl & UF_TA); break;
-        case U_ADD: case U_SUB:
-            read(I.a), read(I.b);
-            trunc = trunc || (I.fl & (UF_TA | UF_TB));
-            break;
-        default: return S;
-        }
-        if (I.d / 8 >= NR) return S;
-        wr[I.d / 8] = 1;
-    }
-    bool all_narrow = true, any_narrow = false;
-    for (size_t k = 0; k < NR; ++k) {
-        if (!wr[k]) continue;
-        const bool n = k < g.narrow.size() && g.narrow[k];
-        all_narrow = all_narrow && n;
-        any_narrow = any_narrow || n;
-    }
-    if (all_narrow) S.mod32 = true;
-    else if (trunc || any_narrow) return S;
-    const uint64_t M = S.mod32 ? 0xffffffffull : ~0ull;
-    std::vector<LinForm> st(NR);
-    std::vector<char> has(NR, 0);
-    auto zero = [&] {
-        LinForm x;
-        x.reg.assign(NR, 0);
-        x.ld.assign(NL, 0);
-        return x;
-    };
-    auto get = [&](uint32_t off) {
-        const uint32_t k = off / 8;
-        if (has[k]) return st[k];
-        LinForm x = zero();
-        x.reg[k] = 1;
-        return x;
-    };
-    auto comb = [&](const LinForm &a, const LinForm &b, uint64_t sb) { // a + sb * b
-        LinForm x = a;
-        for (size_t k = 0; k < NR; ++k) x.reg[k] = (x.reg[k] + sb * b.reg[k]) & M;
-        for (size_t k = 0; k < NL; ++k) x.ld[k] = (x.ld[k] + sb * b.ld[k]) & M;
-        x.c = (x.c + sb * b.c) & M;
-        return x;
-    };
-    for (size_t it = 0; it + 1 < U; ++it) {
-        size_t a = 0;
-        for (size_t pc = r.start; pc < r.start + r.period; ++pc) {
-            const DOp &I = g.D[pc];
-            LinForm x;
-            switch (I.op) {
-            case U_LD: x = zero(); x.ld[it * nlds + a++] = 1; break;
-            case U_LI: x = zero(); x.c = (uint64_t)I.imm & M; break;
-            case U_MOV: x = get(I.a); break;
-            case U_ADDI: x = get(I.a); x.c = (x.c + (uint64_t)I.imm) & M; break;
-            case U_RSUBI: x = comb(zero(), get(I.a), ~0ull); x.c = (x.c + (uint64_t)I.imm) & M; break;
-            case U_ADD: x = comb(get(I.a), get(I.b), 1); break;
-            case U_SUB: x = comb(get(I.a), get(I.b), ~0ull); break;
-            default: return S;
-            }
-            st[I.d / 8] = x;
-            has[I.d / 8] = 1;
-        }
-    }
-    bool chain = false;
-    for (uint32_t k = 0; k < NR; ++k) {
-        if (!(rd[k] && wr[k])) continue;
-        S.carried.push_back(k);
-        S.F.push_back(has[k] ? st[k] : get(k * 8));
-    }
-    for (const LinForm &f : S.F)
-        for (uint32_t k : S.carried) chain = chain || f.reg[k] != 0;
-    S.ok = chain; // nothing to gain without a register carried through the loop
-    return S;
-}
-
-// Source of sum d_i x_i over the block's popped values (x(i) names value i):
-// a balanced tree of multiply-adds when the weights are geometric with the
-// last nonzero weight 1 (sum a^(e-i) x_i), else a balanced sum of products.
-// Each inner node becomes a named temporary (prefix `tp`), so the tree is the
-// dependence structure LLVM sees.
-template <class Name>
-std::string lin_tree(Emitter &e, const std::vector<uint64_t> &d, bool mod32, const Name &x, const std::string &tp)
-{
-    const char *T = mod32 ? "uint32_t" : "uint64_t";
-    const uint64_t M = mod32 ? 0xffffffffull : ~0ull;
-    long lo = -1, hi = -1;
-    for (size_t i = 0; i < d.size(); ++i)
-        if (d[i]) {
-            if (lo < 0) lo = (long)i;
-            hi = (long)i;
-        }
-    if (lo < 0) return "";
-    int tmp = 0;
-    auto lit = [&](uint64_t v) {
-        char b[40];
-        snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull", T, v & M);
-        return std::string(b);
-    };
-    bool geo = d[hi] == 1;
-    const uint64_t a = hi > lo ? d[hi - 1] : 1;
-    for (long i = lo; geo && i < hi; ++i) geo = d[i] != 0 && d[i] == ((a * d[i + 1]) & M);
-    std::function<std::string(long, long)> node;
-    std::vector<uint64_t> pw(hi - lo + 2, 1); // a^k
-    if (geo) {
-        for (size_t k = 1; k < pw.size(); ++k) pw[k] = (pw[k - 1] * a) & M;
-        node = [&](long l, long h) -> std::string {
-            if (l == h) return x(l);
-            const long m = (l + h + 1) / 2;
-            const std::string L = node(l, m - 1), R = node(m, h);
-            const std::string t = tp + std::to_string(tmp++);
-            e.s += "    const " + std::string(T) + " " + t + " = " + (pw[h - m + 1] == 1 ? L : lit(pw[h - m + 1]) + " * " + L) +
-                   " + " + R + ";\n";
-            return t;
-        };
-    } else {
-        node = [&](long l, long h) -> std::string {
-            if (l == h) return d[l] == 0 ? lit(0) : d[l] == 1 ? x(l) : lit(d[l]) + " * " + x(l);
-            const long m = (l + h + 1) / 2;
-            const std::string L = node(l, m - 1), R = node(m, h);
-            const std::string t = tp + std::to_string(tmp++);
-            e.s += "    const " + std::string(T) + " " + t + " = " + L + " + " + R + ";\n";
-            return t;
-        };
-    }
-    return node(lo, hi);
-}
-
 // A rolled loop whose body only reads stack slots (a run of POPs: LD ops, no
 // ST) is software-pipelined: while one block of U iterations uses its
 // popped values, the slots of the next block are already being read, so a
@@ -679,44 +512,8 @@ bool emit_prefetched_run(const OpWriter &w, const Graph &g, const Run &r, std::v
         // keeps the read-ahead here: LLVM otherwise sinks each load to its use
         e.line("    __asm__ volatile(\"\" ::: \"memory\");");
     };
-    const LinSummary lin = g.lim->lin_sum && U >= 4 ? lin_summary(g, r, lds.size(), U) : LinSummary{};
-    int lin_id = 0;
     auto body = [&](char set, const std::string &it) {
-        size_t k0 = 0;
-        if (lin.ok) { // periods 0 .. U-2 of the block in closed form (lin_summary)
-            const char *T = lin.mod32 ? "uint32_t" : "uint64_t";
-            const uint64_t M = lin.mod32 ? 0xffffffffull : ~0ull;
-            const std::string id = std::to_string(D) + "_" + std::to_string(lin_id++);
-            e.line("    {");
-            auto xname = [&](long i) {
-                char b[64];
-                snprintf(b, sizeof b, lin.mod32 ? "(uint32_t)%c%zu_%zu_%zu" : "(uint64_t)(int64_t)%c%zu_%zu_%zu", set, D,
-                         (size_t)i % lds.size(), (size_t)i / lds.size());
-                return std::string(b);
-            };
-            for (size_t q = 0; q < lin.carried.size(); ++q) {
-                const LinForm &f = lin.F[q];
-                std::string x = lin_tree(e, f.ld, lin.mod32, xname, "lt" + id + "_" + std::to_string(q) + "_");
-                for (size_t k = 0; k < f.reg.size(); ++k) {
-                    if (!f.reg[k]) continue;
-                    char b[96];
-                    if (f.reg[k] == 1) snprintf(b, sizeof b, "(%s)%s%zu", T, w.R, k);
-                    else snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull * (%s)%s%zu", T, f.reg[k] & M, T, w.R, k);
-                    x = x.empty() ? std::string(b) : std::string(b) + " + " + x;
-                }
-                if (f.c || x.empty()) {
-                    char b[48];
-                    snprintf(b, sizeof b, "(%s)0x%" PRIx64 "ull", T, f.c & M);
-                    x = x.empty() ? std::string(b) : x + " + " + b;
-                }
-                e.s += "    const " + std::string(T) + " ln" + id + "_" + std::to_string(q) + " = " + x + ";\n";
-            }
-            for (size_t q = 0; q < lin.carried.size(); ++q)
-                e.line("    %s%u = (%s)ln%s_%zu;", w.R, lin.carried[q], lin.mod32 ? "uint32_t" : "int64_t", id.c_str(), q);
-            e.line("    }");
-            k0 = U - 1;
-        }
-        for (size_t k = k0; k < U; ++k) {
+        for (size_t k = 0; k < U; ++k) {
             e.line("    { const uint32_t j%zu = %s + %zuu; (void)j%zu;", D, it.c_str(), k, D);
             for (size_t pc = r.start, a = 0; pc < r.start + r.period; ++pc) {
                 const DOp &I = g.D[pc];
@@ -1359,8 +1156,7 @@ const char *int_flag_fn(const DOp &X, uint32_t v, int ind, size_t body_ops, int6
     return nullptr;
 }
 
-void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc,
-                    const std::string &chain = std::string())
+void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, size_t xpc)
 {
     Emitter &e = w.e;
     const DOp &G = g.D[gpc], &X = g.D[xpc];
@@ -1488,7 +1284,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         if (!g.lim->sat_tier) return;
         e.line("    while (more && T32 - it >= %uu && MK_KEEP(%s > %d, need)) {", 2 * uf, c, uf);
         e.line("    it += %uu;", 2 * uf);
-        if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0)
+        if (uf % (int)g.lim->sat_block == 0)
             for (int u = 0; u < 2 * uf; u += (int)g.lim->sat_block) e.line("    %s = MK_SATDECB(%s);", c, c);
         else
             for (int u = 0; u < 2 * uf; ++u) e.line("    %s = MK_SATDEC(%s);", c, c);
@@ -1538,16 +1334,11 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
             // the whole body is the induction bump: the flag as an int 0/1,
             // no lane masks (mask-writing VALU ops issue at half rate)
             e.line("    int32_t f = 1;");
-            // A countdown by 1 (x > 0, x -= 1): after one iteration a lane
-            // still in the loop has x > 0, so the next x is >= 0 and its flag
-            // is min_u32(x, 1); a lane that left (f = 0) keeps min_u32(x, 0)
-            // = 0.  f = min_u32(x, f) is one VOP2 op where med3 is VOP3
-            // (twice the issue cycles per wave): the first iteration, whose x
-            // may be any value, uses med3 (MK_JIT_FLAG_MIN=0: med3 throughout).
-            const bool fmin = step == -1 && !std::strcmp(flag, "MK_FLAG_GT") && g.lim->flag_min;
+            // A countdown by 1 (x > 0, x -= 1): past its first iteration a
+            // lane still in the loop has x > 0 (sat, below).
             const bool gt = !std::strcmp(flag, "MK_FLAG_GT"), lt = !std::strcmp(flag, "MK_FLAG_LT");
-            if (!fmin && g.lim->sat_count && (g.lim->sat_dec == 1 || g.lim->sat_dec == 3) &&
-                ((gt && step <= -2) || (lt && step >= 1))) {
+            const bool sat = step == -1 && gt;
+            if (!sat && g.lim->sat_count && ((gt && step <= -2) || (lt && step >= 1))) {
                 // Counter form (MK_JIT_SAT_COUNT, round 4): a countdown by k
                 // (x > 0, x -= k; or x < 0, x += k) from x1 after the first
                 // iteration runs z = ceil(|x1| / k) more iterations, so each
@@ -1569,7 +1360,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 emit_sat_tier("z");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
-                if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0) // sat_block decrements per asm block
+                if (uf % (int)g.lim->sat_block == 0) // sat_block decrements per asm block
                     for (int u = 0; u < uf; u += (int)g.lim->sat_block) e.line("    z = MK_SATDECB(z);");
                 else
                     for (int u = 0; u < uf; ++u) e.line("    z = MK_SATDEC(z);");
@@ -1577,7 +1368,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 e.line("    }");
                 e.line("    a = z != 0;");
                 e.line("    x = (int32_t)((uint32_t)x + %uu * (z0 - (uint32_t)z));", (uint32_t)(int32_t)step);
-            } else if (fmin && g.lim->sat_dec) {
+            } else if (sat) {
                 // Past the first iteration a lane still in the loop has x > 0:
                 // one saturating decrement per iteration (v_sub_u32 clamp), a
                 // lane that left holds 0 and its flag is x != 0.  Lanes that
@@ -1587,27 +1378,19 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                 e.line("    (void)f;");
                 e.line("    const int32_t f0 = MK_FLAG_GT(x), x0 = x;");
                 e.line("    x = f0 ? x : 0;");
-                if (g.lim->sat_dec == 2) e.line("    const uint32_t one_ = MK_OPAQUE1();");
                 e.line("    more = MK_KEEP(x != 0, need);");
-                if (g.lim->sat_dec != 2) emit_sat_tier("x");
+                emit_sat_tier("x");
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
-                if (g.lim->sat_dec == 3 && uf % (int)g.lim->sat_block == 0)
+                if (uf % (int)g.lim->sat_block == 0)
                     for (int u = 0; u < uf; u += (int)g.lim->sat_block) e.line("    x = MK_SATDECB(x);");
                 else
-                    for (int u = 0; u < uf; ++u)
-                        e.line(g.lim->sat_dec == 2 ? "    x = MK_SATSUB(x, one_);" : "    x = MK_SATDEC(x);");
+                    for (int u = 0; u < uf; ++u) e.line("    x = MK_SATDEC(x);");
                 e.line("    more = MK_KEEP(x != 0, need);");
                 e.line("    }");
                 e.line("    a = x != 0;");
                 e.line("    x = f0 ? x : x0;");
             } else {
-                if (fmin) {
-                    e.line("    it = 1u;");
-                    e.line("    x = (int32_t)((uint32_t)x - 1u);");
-                    e.line("    f = MK_FLAG_GT(x);");
-                    e.line("    more = MK_KEEP(f != 0, need);");
-                }
                 e.line("    while (more && T32 - it >= %uu) {", uf);
                 e.line("    it += %uu;", uf);
                 for (int u = 0; u < uf; ++u) {
@@ -1615,10 +1398,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
                         e.line("    x = (int32_t)((uint32_t)x %c (uint32_t)f);", step < 0 ? '-' : '+');
                     else
                         e.line("    x = MK_MAD24(f, %d, x);", (int)step);
-                    if (fmin)
-                        e.line("    f = MK_FLAG_MIN(x, f);");
-                    else
-                        e.line("    f = %s(x);", flag);
+                    e.line("    f = %s(x);", flag);
                 }
                 e.line("    more = MK_KEEP(f != 0, need);");
                 e.line("    }");
@@ -1669,20 +1449,8 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         else if (tk != v) cl = "!" + l.cond(X);
     }
     e.line("    L.sb = (a || (%s)) ? (L.steps < lim ? %uu : %uu) : %uu;", cl.c_str(), v, (uint32_t)G.imm, other);
-    e.s += chain;
     e.line("    break;");
     e.line("    }");
-}
-
-// The variant a self-loop leaves to (emit_self_loop's `other`), or ~0u.
-uint32_t loop_exit_target(const Graph &g, uint32_t v, size_t xpc)
-{
-    const DOp &X = g.D[xpc];
-    if (X.op != U_BR) return ~0u;
-    const uint32_t tk = (uint32_t)(uint64_t)X.imm, nt = (uint32_t)((uint64_t)X.imm >> 32);
-    if (tk == v && nt != v) return nt;
-    if (tk != v) return tk;
-    return ~0u;
 }
 
 void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
@@ -1698,7 +1466,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         e.line("#define MK_PRIO_REST()");
         e.line("#endif");
     }
-    if (g.lim->sat_dec == 3) { // host builds: sat_block plain decrements (the device prelude's asm block wins)
+    { // host builds: sat_block plain decrements (the device prelude's asm block wins)
         e.line("#ifndef MK_SATDECB");
         e.line("#define MK_SATDECB(x) ([](int32_t v_) { for (int k_ = 0; k_ < %u; ++k_) v_ = MK_SATDEC(v_); return v_; }(x))",
                g.lim->sat_block);
@@ -1813,83 +1581,6 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         const bool scalar = g.lim->uniform_sw == 1 || (g.lim->uniform_sw < 0 && g.nreach >= 32);
         e.line(scalar ? "#define MK_SCALAR(u) mk_scalar(u)" : "#define MK_SCALAR(u) (u)");
     }
-    // Chaining (round 4, MK_JIT_CHAIN=1; off by default: measured slower, see
-    // JitLimits::chain): a variant whose lanes all go on to
-    // the same next variant w continues there directly (`goto MKV<w>`)
-    // instead of returning to the kernel's dispatcher -- no ballot, readlane
-    // and compare tree for that round.  Only to variants that are not loops
-    // (their unguarded phase needs the wave-wide step maximum, which the
-    // dispatcher computes with the whole wave active) and only along forward
-    // edges of a depth-first order from variant 0, so the gotos add no cycle
-    // and the control flow stays reducible.  A lane that left early (a
-    // budget guard, a side exit) has another L.sb and keeps the chain off
-    // for the group; lanes not in the group wait for the dispatcher as
-    // before.  Sessions keep the plain dispatcher, and so do lanes of more
-    // than 64 reachable variants: the gotos multiply the paths LLVM's
-    // structurizer sees (a 282-variant census network took hiprtc 44 s
-    // without them and over 120 s with them).
-    std::vector<char> is_loop(nv, 0), chain_to(nv, 0), targeted(nv, 0);
-    std::vector<uint32_t> rpo(nv, 0);
-    const bool chain = g.lim->chain && !p.session && g.nreach <= 64;
-    if (chain) {
-        auto succs = [&](uint32_t v, std::vector<uint32_t> &out) {
-            out.clear();
-            for (size_t pc = g.entry[v];; ++pc) {
-                const DOp &I = g.D[pc];
-                if (I.op == U_GUARD || I.op == U_BRX) out.push_back((uint32_t)I.imm);
-                else if (I.op == U_JUMP) { out.push_back((uint32_t)I.imm); break; }
-                else if (I.op == U_BR) {
-                    out.push_back((uint32_t)(uint64_t)I.imm);
-                    out.push_back((uint32_t)((uint64_t)I.imm >> 32));
-                    break;
-                } else if (I.op == U_JRO) {
-                    for (uint64_t t = 0; t <= I.b; ++t) out.push_back(p.jtab[(size_t)I.imm + t]);
-                    break;
-                } else if (I.op == U_END || I.op == U_YIELD || I.op == U_HANDOFF) break;
-            }
-        };
-        // postorder by an explicit stack, then reversed
-        std::vector<char> state(nv, 0);
-        std::vector<uint32_t> post, sv;
-        std::vector<std::pair<uint32_t, size_t>> st{{0u, 0}};
-        std::vector<std::vector<uint32_t>> sc(nv);
-        state[0] = 1;
-        succs(0, sc[0]);
-        while (!st.empty()) {
-            auto &[v, i] = st.back();
-            if (i < sc[v].size()) {
-                const uint32_t t = sc[v][i++];
-                if (t < nv && g.seen[t] && !state[t]) {
-                    state[t] = 1;
-                    succs(t, sc[t]);
-                    st.push_back({t, 0});
-                }
-                continue;
-            }
-            post.push_back(v);
-            st.pop_back();
-        }
-        for (size_t k = 0; k < post.size(); ++k) rpo[post[k]] = (uint32_t)(post.size() - 1 - k);
-        for (uint32_t v = 0; v < nv; ++v) {
-            if (!g.seen[v]) continue;
-            size_t gpc = 0, xpc = 0;
-            is_loop[v] = self_loop(g, v, gpc, xpc);
-            size_t lo, hi;
-            body_range(g, v, lo, hi);
-            const RoundEnds re = round_ends(g, v, lo, hi);
-            const bool checked = !re.segs.empty() && !has_inline_exit(g, lo, hi);
-            chain_to[v] = state[v] && !is_loop[v] && !checked;
-        }
-    }
-    auto chain_line = [&](uint32_t from, uint32_t to) -> std::string {
-        if (!chain || to >= nv || to == from || !chain_to[to] || !g.seen[from] || rpo[to] <= rpo[from]) return "";
-        targeted[to] = 1;
-        char b[96];
-        snprintf(b, sizeof b, "    if (MK_ALL(L.sb == %uu)) goto MKV%u;\n", to, to);
-        return b;
-    };
-    std::string run_src; // mk_run's cases, emitted once the chain targets are known (labels)
-    std::swap(run_src, e.s);
     const size_t fn_start = e.s.size();
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
     e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
@@ -1899,11 +1590,10 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     for (uint32_t v = 0; v < nv; ++v) {
         if (!g.seen[v]) continue;
         e.line("    case %uu: {", v);
-        e.line("    MKL%u_", v); // the chain label, if a chain targets v (resolved below)
         size_t gpc = 0, xpc = 0;
         if (self_loop(g, v, gpc, xpc)) {
             loops.push_back(v);
-            emit_self_loop(w, g, v, gpc, xpc, chain_line(v, loop_exit_target(g, v, xpc)));
+            emit_self_loop(w, g, v, gpc, xpc);
             continue;
         }
         // early exits jump to X<v>, the end of the case
@@ -1942,15 +1632,11 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
         case U_JUMP:
             e.line("    L.steps += %uu;", I.inc);
             e.line("    L.sb = %uu;", (uint32_t)I.imm);
-            e.s += chain_line(v, (uint32_t)I.imm);
             break;
         case U_BR:
             e.line("    L.steps += %uu;", I.inc);
             e.line("    L.sb = %s ? %uu : %uu;", w.cond(I).c_str(), (uint32_t)(uint64_t)I.imm,
                    (uint32_t)((uint64_t)I.imm >> 32));
-            e.s += chain_line(v, (uint32_t)(uint64_t)I.imm);
-            if ((uint32_t)((uint64_t)I.imm >> 32) != (uint32_t)(uint64_t)I.imm)
-                e.s += chain_line(v, (uint32_t)((uint64_t)I.imm >> 32));
             break;
         case U_JRO: {
             e.line("    L.steps += %uu;", I.inc);
@@ -2000,15 +1686,6 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("    }");
     e.line("}");
     e.s.insert(fn_start, tab.s);
-    // chain labels: `MKV<v>: ;` where a chain targets v, nothing elsewhere
-    for (uint32_t v = 0; v < nv; ++v) {
-        const std::string mark = "    MKL" + std::to_string(v) + "_\n";
-        const size_t at = e.s.find(mark);
-        if (at == std::string::npos) continue;
-        e.s.replace(at, mark.size(), targeted[v] ? "    MKV" + std::to_string(v) + ": ;\n" : std::string());
-    }
-    run_src += e.s;
-    std::swap(run_src, e.s);
     e.line("// %zu self-loops", loops.size());
     e.line("MK_FN bool mk_is_loop(const uint32_t u)");
     e.line("{");
@@ -2557,135 +2234,6 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 }
 )";
 
-// Kernel of the machine shape with lanes grouped by value inside each
-// WAVE's share, and no block barriers (MK_JIT_TS_WAVE=1).  Every wave owns a
-// contiguous run of whole 64-input chunks (the same count +-1 for every
-// wave of the grid) and takes it in tiles of at most MK_WS_T inputs:
-//   1. loads them (lane-strided, coalesced), buckets them by value in its
-//      own LDS region: wave min / max, 64 buckets of equal width (a power of
-//      two), a histogram, its prefix sum (one bucket per lane, shuffles) and a
-//      scatter -- a counting sort whose order inside a bucket does not matter;
-//   2. runs them in sorted order, 64 at a time, every chunk by generations;
-//   3. writes each chunk's results straight to their input positions.
-// Nothing waits for another wave: the block-tile kernel's barriers left a
-// wave parked while the slowest wave of its block finished (r04l: 38% of C5's
-// wave cycles in SQ_WAIT_ANY).
-static const char *const kMachineWaveSortKernel = R"(
-#define MK_WS_T (64u * MK_WS_R)
-#define MK_WS_NB 64u
-MK_FN void mk_ws_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
-{
-    __shared__ int32_t s_key[4][MK_WS_T];
-    __shared__ uint16_t s_pos[4][MK_WS_T];
-    __shared__ uint32_t s_cnt[4][MK_WS_NB];
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
-    const uint32_t pol = MK_POLICY;
-    int32_t *const key = s_key[wave];
-    uint16_t *const pos = s_pos[wave];
-    uint32_t *const cnt = s_cnt[wave];
-    uint64_t c_steps = 0u;
-    uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
-    int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
-    const uint64_t gw = (uint64_t)blockIdx.x * 4u + wave, nw = (uint64_t)gridDim.x * 4u;
-    const uint64_t nch = (p.n + 63u) / 64u;
-    const uint64_t c0 = nch * gw / nw, c1 = nch * (gw + 1u) / nw;
-    const uint64_t end = c1 * 64u < p.n ? c1 * 64u : p.n;
-    for (uint64_t base = c0 * 64u; base < end; base += MK_WS_T) {
-        const uint32_t m = end - base < MK_WS_T ? (uint32_t)(end - base) : MK_WS_T;
-        // 1. inputs base + 64 k + lane, their range
-        int32_t v[MK_WS_R];
-        uint32_t lo = 0xFFFFFFFFu, hi = 0u; // biased: signed order as unsigned
-        for (uint32_t k = 0; k < MK_WS_R; ++k) {
-            const uint32_t i = 64u * k + lane;
-            v[k] = i < m ? sched_input(p, base + i) : 0;
-            const uint32_t b = (uint32_t)v[k] ^ 0x80000000u;
-            if (i < m) {
-                lo = b < lo ? b : lo;
-                hi = b > hi ? b : hi;
-            }
-        }
-        lo = MK_WAVE_MIN(lo);
-        hi = MK_WAVE_MAX(hi);
-        const uint32_t span = hi - lo;
-        const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
-        const uint32_t sh = bits > 6u ? bits - 6u : 0u;
-        cnt[lane] = 0u;
-        mk_ws_sync();
-        for (uint32_t k = 0; k < MK_WS_R; ++k) // (buckets recomputed below: fewer registers)
-            if (64u * k + lane < m) atomicAdd(&cnt[(((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh], 1u);
-        mk_ws_sync();
-        {   // exclusive prefix sum over the 64 buckets (lane l owns bucket l)
-            const uint32_t c = cnt[lane];
-            uint32_t x = c;
-            for (uint32_t o = 1u; o < 64u; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-                if (lane >= o) x += y;
-            }
-            mk_ws_sync();
-            cnt[lane] = x - c;
-        }
-        mk_ws_sync();
-        for (uint32_t k = 0; k < MK_WS_R; ++k) {
-            const uint32_t i = 64u * k + lane;
-            if (i >= m) continue;
-            const uint32_t d = atomicAdd(&cnt[(((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh], 1u);
-            key[d] = v[k];
-            pos[d] = (uint16_t)i;
-        }
-        mk_ws_sync();
-        // 2. the sorted lanes, 64 per chunk; 3. results to their input positions
-        const uint32_t nc = (m + 63u) / 64u;
-        for (uint32_t c = 0; c < nc; ++c) {
-            const uint32_t j = c * 64u + lane;
-            const bool live = j < m;
-            MkLane L;
-            mk_init(L, live ? key[j] : 0);
-            const uint32_t at = live ? pos[j] : 0u;
-            if (!live) L.sb = MK_SB_IDLE;
-            for (;;) {
-                const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
-                if (!actb) break;
-                const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
-                const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(L.sb == u ? L.steps : 0u) : 0u;
-                const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
-                if (L.sb == u) mk_run(us, L, p.budget, slots, p.lanes, pol, smax);
-            }
-            if (live) {
-                p.out[base + at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
-                p.status[base + at] = (uint8_t)L.st;
-                if (p.steps) p.steps[base + at] = L.steps;
-            }
-            const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
-            c_steps += (uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps & 0xffffu) : 0u)) +
-                       ((uint64_t)__builtin_amdgcn_readfirstlane(__ockl_wfred_add_u32(live ? (L.steps >> 16) : 0u)) << 16);
-            c_out += (uint32_t)__popcll(__ballot(live && (L.st & MK_ST_HAS_OUTPUT)));
-            c_done += (uint32_t)__popcll(__ballot(live));
-            c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
-            c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
-            c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
-            c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
-        }
-        mk_ws_sync(); // the next tile reuses the wave's LDS
-    }
-    if (p.partials && lane == 0u) { // this wave's row (write_partials' layout)
-        unsigned long long *q = p.partials + (gid >> 6) * 8u;
-        q[0] += c_steps;
-        q[1] += c_out;
-        q[2] += c_done;
-        q[3] += c_qu;
-        q[4] += c_bu;
-        q[5] += c_ov;
-        q[6] += c_os;
-    }
-}
-)";
-
 JitLimits JitLimits::from_env()
 {
     JitLimits l;
@@ -2728,12 +2276,9 @@ JitLimits JitLimits::from_env()
         l.lds_slot_bytes = (size_t)std::strtoull(v, nullptr, 10);
         l.lds_auto = false;
     }
-    flag("MK_JIT_FLAG_MIN", l.flag_min);
-    num("MK_JIT_SAT_DEC", l.sat_dec);
     num("MK_JIT_SAT_BLOCK", l.sat_block);
     if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
     flag("MK_JIT_TS_DYN", l.ts_dyn);
-    flag("MK_JIT_TS_WAVE", l.ts_wave);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
@@ -2742,8 +2287,6 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_LDS_QUAD", l.lds_quad);
     if (const char *v = std::getenv("MK_JIT_UNIFORM_SW"); v && *v) l.uniform_sw = v[0] == '1' ? 1 : v[0] == '0' ? 0 : -1;
     flag("MK_JIT_PROF", l.prof);
-    flag("MK_JIT_LIN_SUM", l.lin_sum);
-    flag("MK_JIT_CHAIN", l.chain);
     flag("MK_JIT_PRIO", l.prio);
     flag("MK_JIT_SAT_TIER", l.sat_tier);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
@@ -2755,22 +2298,17 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,fmin=%d,sdec=%d,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d",
+             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d,sblk=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)flag_min, (int)sat_dec, (int)ts_dyn,
-             (int)tune_regs,
-             lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad);
+             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)ts_dyn,
+             (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
     std::string k = b;
-    if (ts_wave) k += ",tswave=1";
     if (!sat_count) k += ",scount=0";
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
-    if (lin_sum) k += ",lsum=1";
-    if (chain) k += ",chain=1";
     if (!prio) k += ",prio=0";
     if (!sat_tier) k += ",stier=0";
-    if (sat_dec == 3) k += ",sblk=" + std::to_string(sat_block);
     return k;
 }
 
@@ -3103,7 +2641,6 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
         e.line("#define MK_PROF 1");
         e.line("#define MK_T() __builtin_amdgcn_s_memtime()");
     }
-    if (lim.ts_wave) e.line("#define MK_WS_R 12u"); // kMachineWaveSortKernel: a wave's tile, inputs per lane
     e.line("#define MK_ALL(p) (__ballot(!(p)) == 0ull)");
     // MK_JIT_PRIO=1: waves in a self-loop's phases at priority 0, after a
     // loop (dispatch rounds, latency-bound) at 1, so the issue arbiter
@@ -3146,18 +2683,12 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
         e.line("#define MK_SATDEC(x) mk_satdec(x)");
         // sat_block of them in one asm statement: the hazard recognizer's
         // s_nop after an asm statement then comes once per block
-        // (MK_JIT_SAT_DEC=3, MK_JIT_SAT_BLOCK)
-        if (lim.sat_dec == 3) {
-            std::string b = "MK_FN int32_t mk_satdecb(int32_t x) { __asm__(\"";
-            for (uint32_t k = 0; k < lim.sat_block; ++k) b += k ? "\\n\\tv_sub_u32_e64 %0, %0, 1 clamp" : "v_sub_u32_e64 %0, %0, 1 clamp";
-            b += "\" : \"+v\"(x)); return x; }\n";
-            e.s += b;
-        }
+        // (MK_JIT_SAT_BLOCK)
+        std::string b = "MK_FN int32_t mk_satdecb(int32_t x) { __asm__(\"";
+        for (uint32_t k = 0; k < lim.sat_block; ++k) b += k ? "\\n\\tv_sub_u32_e64 %0, %0, 1 clamp" : "v_sub_u32_e64 %0, %0, 1 clamp";
+        b += "\" : \"+v\"(x)); return x; }\n";
+        e.s += b;
         e.line("#define MK_SATDECB(x) mk_satdecb(x)");
-        // the same in plain C, by a 1 that LLVM cannot see (no hazard s_nop after asm)
-        e.line("MK_FN uint32_t mk_opaque1() { uint32_t r; __asm__(\"v_mov_b32 %%0, 1\" : \"=v\"(r)); return r; }");
-        e.line("#define MK_OPAQUE1() mk_opaque1()");
-        e.line("#define MK_SATSUB(x, o) ((int32_t)__builtin_elementwise_sub_sat((uint32_t)(x), (o)))");
     }
     // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
     if (lim.slot_nt) {
@@ -3281,7 +2812,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
     Emitter e;
     e.s = module_prelude(shape, lim, pool, lane_src.find("MK_SAT") != std::string::npos);
     e.s += lane_src;
-    const char *mk = lim.tile_sort && !lim.order ? (lim.ts_wave ? kMachineWaveSortKernel : kMachineSortKernel)
+    const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel
                                                  : kMachineKernel;
     if (shape == JIT_MACHINE && pool >= 64) mk = kMachinePoolKernel;
     else if (shape == JIT_MACHINE && pool >= 2) mk = kMachineMultiKernel;

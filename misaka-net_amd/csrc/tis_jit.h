@@ -117,9 +117,6 @@ struct JitLimits {
     // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
     // order.
     bool ts_dyn = false;
-    // Its variant without block barriers: each wave sorts and runs its own
-    // contiguous share (MK_JIT_TS_WAVE=1, kMachineWaveSortKernel).
-    bool ts_wave = false;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
@@ -128,19 +125,14 @@ struct JitLimits {
     // The loader picks each heavy network's LDS budget and register count
     // (mk_exec.hip tune_soft_regs) unless MK_JIT_LDS_SLOTS sets the budget.
     bool lds_auto = true;
-    // Machine-shape countdown loops (x > 0, x -= 1) keep their int flag by
-    // min_u32(x, f), a VOP2 op, after a first iteration by med3 (VOP3)
-    // (MK_JIT_FLAG_MIN=0: med3 in every iteration).
-    bool flag_min = true;
-    // ... and, past that first iteration, run as one saturating decrement per
-    // iteration (v_sub_u32 x, x, 1 clamp: a lane that left holds 0), the
-    // flag being x != 0 (MK_JIT_SAT_DEC=0: sub + min_u32 per iteration;
-    // 1: inline asm; 2: LLVM's usub.sat by an opaque 1, no hazard s_nop).
-    // 3 (default since round 4): as 1 with MK_JIT_SAT_BLOCK (4, 8, 16, 32)
-    // decrements per asm statement, so the hazard recognizer's s_nop after an
-    // asm statement comes once per block (r05h, C5 launch: block 4 120.6 us,
-    // 8 121.9, 16 121.6, 32 122.9, one per statement 125.2-125.6).
-    uint32_t sat_dec = 3;
+    // Machine-shape countdown loops (x > 0, x -= 1) run, past their first
+    // iteration, as one saturating decrement per iteration (v_sub_u32 x, x, 1
+    // clamp: a lane that left holds 0), the flag being x != 0, with
+    // MK_JIT_SAT_BLOCK (4, 8, 16, 32) decrements per asm statement, so the
+    // hazard recognizer's s_nop after an asm statement comes once per block
+    // (r05h, C5 launch: block 4 120.6 us, 8 121.9, 16 121.6, 32 122.9, one
+    // per statement 125.2-125.6).  Round 5 removed the superseded forms
+    // (sub + min_u32 flags, one decrement per statement, usub.sat).
     uint32_t sat_block = 4;
     // ... and a countdown by any other step k (x > 0, x -= k; x < 0, x += k)
     // as one saturating decrement of its remaining-iteration count per
@@ -175,21 +167,6 @@ struct JitLimits {
     // dispatch rounds in place of the launch's counters (MK_JIT_PROF=1;
     // tools/probe/c5_decomp.py).  The launch's statistics are then not counts.
     bool prof = false;
-    // Pop runs whose register updates are linear run each prefetched block's
-    // first periods in closed form, the popped values combined by a tree
-    // (tis_jit.cpp lin_summary; MK_JIT_LIN_SUM=1).  Bit-exact, and measured
-    // neutral (r04w: C4 d256 158.1 vs 159.9 us, d1024 2,324 vs 2,320 us): at
-    // one wave per SIMD a wave issues one VALU op per ~8.8 cycles whether or
-    // not it depends on the previous one (tools/probe/valu_rates.hip), so a
-    // shorter chain of the same ops does not shorten the wave.  Off.
-    bool lin_sum = false;
-    // Machine lanes continue straight into the next variant when all of a
-    // group's lanes go there (tis_jit.cpp emit_machine_lane; MK_JIT_CHAIN=1).
-    // Measured slower (r05d, launch times, chained vs dispatcher): C5 139.9 vs
-    // 123.5 us (77 -> 83 VGPRs), two_stacks 242.3 vs 230.1, dyn_depth 136.3
-    // vs 132.9 -- the extra paths cost more than the dispatch rounds saved.
-    // Off.
-    bool chain = false;
     // Wave priority: 0 inside self-loops, 1 after them (module_prelude;
     // MK_JIT_PRIO=0: none).  The issue arbiter then prefers the dispatch
     // rounds' latency-bound waves over the loops' VALU streams (r05o, C5

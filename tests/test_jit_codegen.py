@@ -141,19 +141,16 @@ def test_loop_phases(tmp_path):
     assert len(check_cases(tmp_path, cases, machine=True)) == len(cases)
 
 
-# The countdown's saturating-decrement forms (MK_JIT_SAT_DEC: 0 sub + min_u32,
-# 2 usub.sat by an opaque 1; the default 1 runs in every other test) and the
-# counter form of countdowns by other steps (MK_JIT_SAT_COUNT, default on;
-# "count0" turns it off): every loop path, and C5 over all trip counts and at
-# budgets inside its loops.
-@pytest.mark.parametrize("mode", ["0", "1", "2", "count0", "b32", "default"])
+# The countdown's saturating decrements in asm blocks of MK_JIT_SAT_BLOCK
+# (default 4) and the counter form of countdowns by other steps
+# (MK_JIT_SAT_COUNT, default on; "count0" turns it off): every loop path, and
+# C5 over all trip counts and at budgets inside its loops.
+@pytest.mark.parametrize("mode", ["count0", "b8", "b32", "default"])
 def test_countdown_forms(tmp_path, monkeypatch, mode):
     if mode == "count0":
         monkeypatch.setenv("MK_JIT_SAT_COUNT", "0")
-    elif mode.startswith("b"):  # the default form (3) with other asm block sizes
+    elif mode.startswith("b"):  # other asm block sizes
         monkeypatch.setenv("MK_JIT_SAT_BLOCK", mode[1:])
-    elif mode != "default":
-        monkeypatch.setenv("MK_JIT_SAT_DEC", mode)
     cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
     cases.append(("c5_all_trips", mk.networks.countdown_network(), np.arange(-3, 1024, dtype=np.int64), {}))
     for b in (1, 2, 3, 37, 400, 1500):
@@ -358,40 +355,14 @@ POP_CHAINS = {
 }
 
 
-@pytest.mark.parametrize("lin", ["1", "0"])
 @pytest.mark.parametrize("tail", ["out", "sign"])
-def test_pop_chain_closed_form(tmp_path, monkeypatch, lin, tail):
-    """Pop runs in closed form (tis_jit.cpp lin_summary, MK_JIT_LIN_SUM): every
-    linear accumulation, read only through hops (narrow: mod 2^32) or by a
-    sign test (wide: mod 2^64, no truncating operand), bit-exact against the
-    oracle on full-range inputs (INT32_MIN/MAX included), with the closed
-    form present in the source where it applies."""
-    monkeypatch.setenv("MK_JIT_LIN_SUM", lin)
+def test_pop_chains(tmp_path, tail):
+    """Pipelined pop runs (emit_prefetched_run) feeding linear accumulations,
+    read through hops (narrow registers) or by a sign test (wide), bit-exact
+    against the oracle on full-range inputs (INT32_MIN/MAX included)."""
     t = "SWP\nOUT ACC" if tail == "out" else "SWP\nJGZ P\nOUT 1\nJMP E\nP: OUT ACC\nE: NOP"
-    cases, srcs = [], {}
+    cases = []
     for name, accum in POP_CHAINS.items():
         nodes = [NodeSpec("a", "program", _pop_chain_program(accum, 100, t)), NodeSpec("s", "stack", "")]
         cases.append((f"{name}-{tail}", nodes, po.gen_inputs(SEED, 300), {}))
-        srcs[name] = sc.jit_lane(nodes)[0]
     check_cases(tmp_path, cases)
-    closed = {n for n, s in srcs.items() if "const uint32_t ln" in s or "const uint64_t ln" in s}
-    if lin == "0":
-        assert not closed
-    elif tail == "out":  # narrow accumulators: every chain in closed form
-        assert closed == set(POP_CHAINS), closed
-    else:
-        assert closed, "no wide chain in closed form"
-
-
-def test_chained_variants(tmp_path, monkeypatch):
-    """Opt-in variant chaining (MK_JIT_CHAIN=1, emit_machine_lane): the
-    machine lane's gotos between variants, on the configs and random
-    networks, bit-exact against the oracle; the chains are present."""
-    monkeypatch.setenv("MK_JIT_CHAIN", "1")
-    cases = [("c5", mk.networks.countdown_network(), po.gen_inputs(SEED, 1500, kind=1, mask=1023), {}),
-             ("c5_budget", mk.networks.countdown_network(), po.gen_inputs(SEED, 600, kind=1, mask=1023),
-              {"budget": 777})]
-    for seed in (3, 5, 9, 17, 41):
-        cases.append((f"seed{seed}", random_network(seed), po.gen_inputs(seed, 300), {"budget": [97, 5000][seed % 2]}))
-    check_cases(tmp_path, cases, machine=True)
-    assert "goto MKV" in sc.jit_lane(mk.networks.countdown_network(), machine=True)[0]

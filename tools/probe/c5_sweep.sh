@@ -14,7 +14,7 @@ P="python -u tools/probe/c5_decomp.py"
 for m in 0 1 15 63 255 1023 4095; do
   timeout -k 10 120 $P $m | tee -a "$OUT/masks.jsonl"
 done
-for kv in MK_JIT_UNIFORM_SW=0 MK_JIT_SAT_DEC=2 MK_JIT_TS_WAVES=8 MK_JIT_TS_ROUNDS=8 MK_JIT_TS_DYN=1 MK_JIT_LOOP_UNROLL=16 \
+for kv in MK_JIT_UNIFORM_SW=0 MK_JIT_TS_WAVES=8 MK_JIT_TS_ROUNDS=8 MK_JIT_TS_DYN=1 MK_JIT_LOOP_UNROLL=16 \
           MK_JIT_LOOP_UNROLL=64; do
   export "$kv"
   timeout -k 10 120 $P 1023 | tee -a "$OUT/knobs.jsonl"
