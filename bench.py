@@ -223,6 +223,26 @@ def measured_traffic(workload):
     return measured_profile(workload).get("hbm_bytes_per_launch")
 
 
+def occupancy_cap(waves_per_simd):
+    """Measured VALU issue cap at this many resident waves per SIMD: the best
+    rate over independent chains of full-rate int ops in
+    profiles/r04n_valu_rates.jsonl (tools/probe/valu_rates.hip, MI355X), at
+    the largest measured occupancy not above it.  None without a match."""
+    p = os.path.join(ROOT, "profiles", "r04n_valu_rates.jsonl")
+    if not waves_per_simd or not os.path.exists(p):
+        return None
+    rows = [json.loads(line) for line in open(p) if line.strip()]
+    rows = [r for r in rows if r["op"] in ("add_u32_vop2", "sub_clamp_vop3")]
+    ws = [r["waves_per_simd"] for r in rows if r["waves_per_simd"] <= waves_per_simd]
+    if not ws:
+        return None
+    w = max(ws)
+    best = max((r for r in rows if r["waves_per_simd"] == w), key=lambda r: r["T_lane_ops"])
+    return {"waves_per_simd": waves_per_simd, "measured_at_waves_per_simd": w, "cap": best["T_lane_ops"],
+            "unit": "Tlane-op/s", "op": best["op"], "chains": best["chains"],
+            "source": "profiles/r04n_valu_rates.jsonl"}
+
+
 def valu_peak(stream):
     """Live dependency-free v_add_u32 probe on this GPU (lane-ops/s)."""
     blocks, iters = 256 * 8 * 4, 2000
@@ -651,6 +671,14 @@ def main():
             "launch_us": launch_max * 1e6,
             "counter_source": prof.get("source"),
         }
+        # the same executed rate against what a kernel at this occupancy can
+        # issue (one wave per SIMD issues a VALU op only
+        # every ~8.8 cycles), reproducible from profiles/
+        m = re.search(r"waves_per_simd=(\d+)", plan)
+        occ = occupancy_cap(int(m.group(1)) if m else 0)
+        if occ:
+            occ["frac"] = issue["achieved"] / occ["cap"]
+        issue["occupancy"] = occ
     else:
         # No PMC profile of this kernel: the executed work is unknown.  The
         # frozen k = 4 model is reported beside it,

@@ -3955,6 +3955,14 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
             s += " chunk=" + std::to_string(std::max<uint64_t>(blk, fit / blk * blk));
         }
         s += " knobs=" + h->jit_lim.key();
+        // resident waves per SIMD of the loaded kernel (registers and LDS;
+        // the first device it is loaded on): the occupancy its issue rate is
+        // priced at (bench.py roofline_issue.occupancy)
+        for (int d = 0; d < mk::kMaxDevices; d++)
+            if (sc->jit.dev[d].fn) {
+                s += " waves_per_simd=" + std::to_string(sc->jit.dev[d].per_cu * sc->jit.block / 256);
+                break;
+            }
     } else {
         const bool tile = (flags & MK_FLAG_TILE) ? true : (flags & MK_FLAG_REFILL) ? false : sc->tile;
         uint32_t B, K;

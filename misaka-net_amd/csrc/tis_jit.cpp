@@ -2021,6 +2021,8 @@ static const char *const kMachineSortKernel = R"(
 // lane states (C5 at 8: 79 -> 63 VGPRs, yet 220 vs 215 us: off by default).
 #if MK_LANE_REGS <= 8 && MK_TS_WAVES_N
 #define MK_TS_WAVES __attribute__((amdgpu_waves_per_eu(MK_TS_WAVES_N)))
+#elif MK_LANE_REGS <= 8 && defined(MK_TS_VGPRS_N)
+#define MK_TS_WAVES __attribute__((amdgpu_num_vgpr(MK_TS_VGPRS_N)))
 #else
 #define MK_TS_WAVES
 #endif
@@ -2271,6 +2273,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
     num("MK_JIT_TS_WAVES", l.ts_waves);
+    num("MK_JIT_TS_VGPRS", l.ts_vgprs);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
     if (const char *v = std::getenv("MK_JIT_LDS_SLOTS"); v && *v) {
         l.lds_slot_bytes = (size_t)std::strtoull(v, nullptr, 10);
@@ -2305,6 +2308,7 @@ std::string JitLimits::key() const
              (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
     std::string k = b;
     if (!sat_count) k += ",scount=0";
+    if (ts_vgprs) k += ",tsv=" + std::to_string(ts_vgprs);
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
     if (!prio) k += ",prio=0";
@@ -2634,6 +2638,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
+    if (lim.ts_vgprs) e.line("#define MK_TS_VGPRS_N %u", lim.ts_vgprs); // its VGPR bound (experiment)
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
