@@ -1585,48 +1585,22 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("MK_FN void mk_run(const uint32_t u, MkLane &L, const uint32_t budget, int32_t *__restrict__ slots,");
     e.line("                  const uint64_t sstride, const uint32_t pol, const uint32_t smax)");
     e.line("{");
-    e.line("    (void)slots; (void)sstride; (void)budget; (void)pol; (void)smax;");
-    e.line("    switch (u) {");
-    for (uint32_t v = 0; v < nv; ++v) {
-        if (!g.seen[v]) continue;
-        e.line("    case %uu: {", v);
-        size_t gpc = 0, xpc = 0;
-        if (self_loop(g, v, gpc, xpc)) {
-            loops.push_back(v);
-            emit_self_loop(w, g, v, gpc, xpc);
-            continue;
-        }
-        // early exits jump to X<v>, the end of the case
+    // Variant v's code (guard, body, exit op) up to the label `lab:`, its
+    // early exits jumping there.
+    auto emit_plain = [&](uint32_t v, const std::string &lab) {
         const DOp &G = g.D[g.entry[v]];
         if (G.op == U_GUARD) {
             e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", G.inc);
             e.line("        L.sb = %uu;", (uint32_t)G.imm);
-            e.line("        goto X%u;", v);
+            e.line("        goto %s;", lab.c_str());
             e.line("    }");
         }
         size_t lo, hi;
         body_range(g, v, lo, hi);
-        const RoundEnds re = round_ends(g, v, lo, hi);
-        if (!re.segs.empty() && !has_inline_exit(g, lo, hi)) { // checked variant: always ends at a round end (emit_budget_exit)
-            e.line("    int32_t mk_o = 0;");
-            emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
-                if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
-            });
-            emit_budget_exit(e, tab, re, v, "L.steps");
-            e.line("    L.steps += inc_;");
-            e.line("    L.st = st_;");
-            e.line("    L.outv = (st_ & %uu) ? mk_o : 0;", (unsigned)MK_ST_HAS_OUTPUT);
-            e.line("    L.sb = MK_SB_DONE;");
-            e.line("    (void)mk_o;");
-            e.line("    X%u:", v);
-            e.line("    break;");
-            e.line("    }");
-            continue;
-        }
-        char fin[48], go[48];
-        snprintf(fin, sizeof fin, "L.sb = MK_SB_DONE; goto X%u;", v);
-        snprintf(go, sizeof go, "L.sb = %%uu; goto X%u;", v);
-        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) { emit_inline_end(w, I, inc, "L.", fin, go); });
+        const std::string fin = "L.sb = MK_SB_DONE; goto " + lab + ";", go = "L.sb = %uu; goto " + lab + ";";
+        emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *inc, size_t) {
+            emit_inline_end(w, I, inc, "L.", fin.c_str(), go.c_str());
+        });
         const DOp &I = g.D[hi];
         switch (I.op) {
         case U_JUMP:
@@ -1678,7 +1652,46 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             break;
         default: break;
         }
-        e.line("    X%u:", v);
+        e.line("    %s:", lab.c_str());
+    };
+    e.line("    (void)slots; (void)sstride; (void)budget; (void)pol; (void)smax;");
+    e.line("    switch (u) {");
+    for (uint32_t v = 0; v < nv; ++v) {
+        if (!g.seen[v]) continue;
+        e.line("    case %uu: {", v);
+        size_t gpc = 0, xpc = 0;
+        if (self_loop(g, v, gpc, xpc)) {
+            loops.push_back(v);
+            emit_self_loop(w, g, v, gpc, xpc);
+            continue;
+        }
+        size_t lo, hi;
+        body_range(g, v, lo, hi);
+        const RoundEnds re = round_ends(g, v, lo, hi);
+        if (!re.segs.empty() && !has_inline_exit(g, lo, hi)) { // checked variant: always ends at a round end (emit_budget_exit)
+            const DOp &G = g.D[g.entry[v]];
+            if (G.op == U_GUARD) {
+                e.line("    if ((uint64_t)L.steps + %uu >= (uint64_t)budget) {", G.inc);
+                e.line("        L.sb = %uu;", (uint32_t)G.imm);
+                e.line("        goto X%u;", v);
+                e.line("    }");
+            }
+            e.line("    int32_t mk_o = 0;");
+            emit_body(w, g, v, lo, hi, [&](const DOp &I, const char *, size_t pc) {
+                if (pc == re.snap_pc) e.line("    mk_o = %s;", w.result(I).c_str());
+            });
+            emit_budget_exit(e, tab, re, v, "L.steps");
+            e.line("    L.steps += inc_;");
+            e.line("    L.st = st_;");
+            e.line("    L.outv = (st_ & %uu) ? mk_o : 0;", (unsigned)MK_ST_HAS_OUTPUT);
+            e.line("    L.sb = MK_SB_DONE;");
+            e.line("    (void)mk_o;");
+            e.line("    X%u:", v);
+            e.line("    break;");
+            e.line("    }");
+            continue;
+        }
+        emit_plain(v, "X" + std::to_string(v));
         e.line("    break;");
         e.line("    }");
     }
@@ -2021,8 +2034,6 @@ static const char *const kMachineSortKernel = R"(
 // lane states (C5 at 8: 79 -> 63 VGPRs, yet 220 vs 215 us: off by default).
 #if MK_LANE_REGS <= 8 && MK_TS_WAVES_N
 #define MK_TS_WAVES __attribute__((amdgpu_waves_per_eu(MK_TS_WAVES_N)))
-#elif MK_LANE_REGS <= 8 && defined(MK_TS_VGPRS_N)
-#define MK_TS_WAVES __attribute__((amdgpu_num_vgpr(MK_TS_VGPRS_N)))
 #else
 #define MK_TS_WAVES
 #endif
@@ -2273,7 +2284,6 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
     num("MK_JIT_TS_WAVES", l.ts_waves);
-    num("MK_JIT_TS_VGPRS", l.ts_vgprs);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
     if (const char *v = std::getenv("MK_JIT_LDS_SLOTS"); v && *v) {
         l.lds_slot_bytes = (size_t)std::strtoull(v, nullptr, 10);
@@ -2308,7 +2318,7 @@ std::string JitLimits::key() const
              (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
     std::string k = b;
     if (!sat_count) k += ",scount=0";
-    if (ts_vgprs) k += ",tsv=" + std::to_string(ts_vgprs);
+
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
     if (!prio) k += ",prio=0";
@@ -2638,7 +2648,6 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
     e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
-    if (lim.ts_vgprs) e.line("#define MK_TS_VGPRS_N %u", lim.ts_vgprs); // its VGPR bound (experiment)
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves

@@ -102,7 +102,6 @@ struct JitLimits {
     // the register allocator, MK_JIT_TS_WAVES; 0: the compiler's choice --
     // measured best: C5 215 us vs 220 at 8 and 243 at 6, r02l).
     uint32_t ts_waves = 0;
-    uint32_t ts_vgprs = 0; // MK_JIT_TS_VGPRS: amdgpu_num_vgpr bound instead (experiment)
     // Its tile: 256 x ts_rounds inputs, each wave running ts_rounds sorted
     // chunks of 64 per tile (MK_JIT_TS_ROUNDS = 4, 8 or 16).  r02v: 8 is 2%
     // faster on C5 (211 vs 215 us) but 20% / 8% slower on the dynamic-stack
