@@ -1540,6 +1540,16 @@ struct JitState {
     JitDev dev[kMaxDevices];
 };
 
+// One way to run a heavy stream network with stack slots (tune_lds_auto):
+// its schedule, LDS bytes of slots per wave, micro-op bound, and the waves
+// per SIMD it is meant for (0: none checked).
+struct StackPlan {
+    SchedProgram prog;
+    size_t lds_bytes = 0;
+    size_t max_dops = 0;
+    uint32_t waves = 0;
+};
+
 // A compiled schedule for one (stack_cap, stop_on_output) pair.
 struct SchedCache {
     uint32_t cap = 0;
@@ -1548,6 +1558,10 @@ struct SchedCache {
     bool tile = false; // default lane scheduling (sched_default_tile)
     bool lds_set = false;   // tune_soft_regs chose the heavy kernel's LDS budget ...
     size_t lds_bytes = 0;   // ... this many bytes of slots per wave (0: slots in HBM)
+    size_t max_dops = 0;    // ... and a larger micro-op bound for its unrolled register entries (0: the knob's)
+    uint32_t want_waves = 0;  // waves per SIMD the schedule is for: its module's registers are checked (0: none)
+    std::vector<StackPlan> alts; // the next plans to try when that check fails (tune_lds_auto)
+    std::string occ_note;     // what the check found (mk_net_plan occupancy=)
     std::string why;
     SchedProgram prog;
     SchedDev dev[kMaxDevices];
@@ -1809,6 +1823,70 @@ bool heavy_stream(const SchedProgram &P, const JitLimits &jl)
     return jit_lane_source(P, jl, src, why, &shape, nullptr, &heavy) && shape == JIT_STREAM && heavy;
 }
 
+// More waves per SIMD for heavy LDS networks (round 5).  At one wave per
+// SIMD a gfx950 wave issues a VALU op only every ~8.8 cycles; C4 D=256's
+// default kernel (64 registers, 160 of 193 slots in LDS, one wave per SIMD)
+// spent its time there (profiles/r06b_pmc_stall_c4d256_c5.txt).  Keeping more
+// stack entries in registers (SchedLimits::soft_regs) leaves fewer slots, and
+// W waves per SIMD leave each wave 160 KiB / 4W of LDS.  For W = 8 and then
+// 2, a register count up to kStackRegs that puts every slot in that share
+// makes a plan, with a micro-op bound of kStackDops for the unrolled
+// register entries.  Registers are the risk: a program whose register-held
+// entries stay live needs more VGPRs than W waves allow, so jit_compile
+// checks the compiled module (vgprs, agprs, scratch) against W and falls back
+// to the next plan, and last to the one-wave default (which is not checked).
+// Measured on MI355X (r06f/r06g, C4 D=256, 512K lanes): the default 159.8 us;
+// two waves, 80 slots in LDS, 128 / 144 / 152 / 176 registers (49 / 33 / 25 /
+// 1 slots left in HBM) 126.5 / 80.3 / 69.5 / 55.0 us; three waves (208
+// registers, 48 slots in LDS) 13.9 us.  With the stack entries in registers
+// LLVM sees the pushed values and folds the pipeline's pop chains, so the
+// stack traffic per PUSH/POP falls with the registers (bench.py reports it,
+// `stack.stack_ops_executed_per_push_pop`).
+constexpr uint32_t kStackRegs = 256;
+constexpr size_t kStackDops = 16384;
+
+std::vector<StackPlan> more_waves(mk_net *h, SchedCache *sc, const SchedLimits &lim0, uint32_t regs0, uint32_t slots0)
+{
+    std::vector<StackPlan> out;
+    const JitLimits &jl = h->jit_lim;
+    if (!jl.lds_slot_bytes || jl.lds_quad) return out;
+    JitLimits jl2 = jl;
+    jl2.max_dops = std::max(jl.max_dops, kStackDops);
+    // Each added register takes about one slot (an entry of the deepest
+    // stack window): start at the count that predicts a fit and step up.
+    // compile_schedule takes seconds on deep pipelines, so few probes.
+    for (uint32_t waves : {8u, 2u}) {
+        const uint64_t cap = std::min<uint64_t>(jl.lds_slot_bytes, (160u * 1024u) / (4u * waves) / 2048u * 2048u);
+        const uint32_t k = (uint32_t)(cap / 256u); // slots of a wave's LDS share
+        if (slots0 <= k) continue;
+        for (uint32_t r = regs0 + (slots0 - k), probes = 0; r <= kStackRegs && probes < 4; r += 4u, ++probes) {
+            SchedLimits l = lim0;
+            l.soft_regs = r;
+            l.max_regs = std::max(l.max_regs, r + 24u);
+            StackPlan sp;
+            std::string w;
+            if (!compile_schedule(h->net, sc->cap, sc->soo, l, sp.prog, w) || !heavy_stream(sp.prog, jl2)) break;
+            if (sp.prog.nslots > k) continue;
+            sp.lds_bytes = (size_t)cap;
+            sp.max_dops = jl2.max_dops;
+            sp.waves = waves;
+            out.push_back(std::move(sp));
+            break;
+        }
+    }
+    return out;
+}
+
+// Installs a plan (a tuning choice, or the next after a failed check).
+void use_plan(SchedCache *sc, StackPlan &&sp)
+{
+    sc->prog = std::move(sp.prog);
+    sc->lds_set = true;
+    sc->lds_bytes = sp.lds_bytes;
+    sc->max_dops = sp.max_dops;
+    sc->want_waves = sp.waves;
+}
+
 // Default policy for heavy stream networks (JitLimits::lds_auto): waves per
 // CU first, then as many slots in LDS as those waves leave room for.
 //   * slots that fit LDS at four waves per CU at the default registers: keep
@@ -1849,9 +1927,17 @@ void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
                 break;
             }
         }
-    sc->prog = std::move(best);
-    sc->lds_set = true;
-    sc->lds_bytes = budget;
+    std::vector<StackPlan> more = more_waves(h, sc, lim0, best.nregs, best.nslots);
+    StackPlan def;
+    def.prog = std::move(best);
+    def.lds_bytes = budget;
+    if (more.empty()) {
+        use_plan(sc, std::move(def));
+        return;
+    }
+    for (size_t k = 1; k < more.size(); ++k) sc->alts.push_back(std::move(more[k]));
+    sc->alts.push_back(std::move(def));
+    use_plan(sc, std::move(more[0]));
 }
 
 // MK_JIT_LDS_SLOTS set: registers for the fixed LDS budget (see above).
@@ -2720,11 +2806,71 @@ bool rtc_compile(const std::string &src, double max_s, std::vector<char> &code, 
     return true;
 }
 
+// A numeric field of a code object's AMDGPU metadata (the msgpack note:
+// ".vgpr_count", ".agpr_count", ".private_segment_fixed_size"; the native
+// modules hold one kernel), or -1.
+int64_t co_meta(const std::vector<char> &co, const char *key)
+{
+    const size_t n = std::strlen(key);
+    if (!n || n > 31) return -1;
+    const std::string pat = std::string(1, (char)(0xa0u | (unsigned)n)) + key, img(co.begin(), co.end());
+    const size_t at = img.find(pat);
+    if (at == std::string::npos || at + pat.size() >= img.size()) return -1;
+    const size_t i = at + pat.size();
+    const uint8_t b = (uint8_t)img[i];
+    auto be = [&](size_t k) -> int64_t {
+        if (i + k >= img.size()) return -1;
+        uint64_t v = 0;
+        for (size_t j = 1; j <= k; ++j) v = v << 8 | (uint8_t)img[i + j];
+        return (int64_t)v;
+    };
+    if (b < 0x80u) return b;
+    if (b == 0xccu) return be(1);
+    if (b == 0xcdu) return be(2);
+    if (b == 0xceu) return be(4);
+    return -1;
+}
+
+// Whether a module holds `waves` waves per SIMD: VGPRs + AGPRs in 8-register
+// granules within gfx950's 512 per SIMD lane, and no scratch.  `note` says
+// what was found.
+bool module_holds(const std::vector<char> &co, uint32_t waves, std::string &note)
+{
+    const int64_t v = co_meta(co, ".vgpr_count"), a = co_meta(co, ".agpr_count"),
+                  ps = co_meta(co, ".private_segment_fixed_size");
+    const int64_t alloc = (v + 7) / 8 * 8 + (std::max<int64_t>(a, 0) + 7) / 8 * 8;
+    char b[96];
+    snprintf(b, sizeof b, "w%u:v%lld,a%lld,s%lld", waves, (long long)v, (long long)a, (long long)ps);
+    note = b;
+    return v >= 0 && ps == 0 && alloc * (int64_t)waves <= 512;
+}
+
+// Drops a SchedCache's tier-2 device code and slots (after its schedule
+// changed; rebuilt on next use).  Caller holds h->mu.
+void drop_sched_devices(SchedCache *sc)
+{
+    for (int d = 0; d < kMaxDevices; d++) {
+        SchedDev &sd = sc->dev[d];
+        if (!sd.d_code && !sd.d_slots && !sd.d_order) continue;
+        DeviceGuard g(d);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(sd.d_code);
+        (void)hipFree(sd.d_entry);
+        (void)hipFree(sd.d_jtab);
+        (void)hipFree(sd.d_slots);
+        (void)hipFree(sd.d_order);
+        (void)hipFree(sd.d_ordtab);
+        sd = SchedDev{};
+    }
+}
+
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
 // gfx950); the code object is loaded per device on first use.  Bounded:
 // a lane source over lim.max_src_bytes is not compiled, and a compile that
 // takes longer than lim.max_compile_s is abandoned -- either way the
-// network stays on tier 2 with the reason in mk_net_plan.
+// network stays on tier 2 with the reason in mk_net_plan.  A schedule tuned
+// for more waves per SIMD (StackPlan::waves) whose module cannot hold them
+// (or does not compile) gives way to the next plan (more_waves).
 bool jit_compile(SchedCache *sc, const JitLimits &lim)
 {
     JitState &J = sc->jit;
@@ -2739,28 +2885,51 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
         return false;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    JitLimits L = lim; // the network's LDS budget, when the loader chose one (tune_lds_auto)
-    if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
-    std::string lane;
-    if (!jit_lane_source(sc->prog, L, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool)) return false;
-    J.heavy = J.heavy && J.shape == JIT_STREAM;
-    J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, L);
-    J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, L) : 0u;
-    J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
-    const std::string src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
-    J.src_bytes = src.size();
-    J.src_hash = src_hash(src);
-    if (!rtc_compile(src, lim.max_compile_s, J.code, J.why, J.rtc)) return false;
-    if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded,
-        if (FILE *f = std::fopen(d, "wb")) {                   // and its source beside it (<path>.hip)
-            std::fwrite(J.code.data(), 1, J.code.size(), f);
-            std::fclose(f);
+    for (;;) {
+        JitLimits L = lim; // the network's LDS budget, when the loader chose one (tune_lds_auto)
+        if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
+        if (sc->max_dops) L.max_dops = std::max(L.max_dops, sc->max_dops);
+        std::string lane, note;
+        bool ok = jit_lane_source(sc->prog, L, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool);
+        std::string src;
+        if (ok) {
+            J.heavy = J.heavy && J.shape == JIT_STREAM;
+            J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, L);
+            J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, L) : 0u;
+            J.block = J.heavy ? kJitHeavyBlock : J.pool >= 64 ? kJitPoolBlock : kJitBlock;
+            src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
+            J.src_bytes = src.size();
+            J.src_hash = src_hash(src);
+            ok = rtc_compile(src, lim.max_compile_s, J.code, J.why, J.rtc);
         }
-        if (FILE *f = std::fopen((std::string(d) + ".hip").c_str(), "wb")) {
-            std::fwrite(src.data(), 1, src.size(), f);
-            std::fclose(f);
+        if (sc->want_waves) {
+            const bool held = ok && module_holds(J.code, sc->want_waves, note);
+            sc->occ_note += (sc->occ_note.empty() ? "" : ";") + (ok ? note : "w" + std::to_string(sc->want_waves) + ":declined") +
+                            (held ? "" : "-rejected");
+            if (!held && !sc->alts.empty()) { // the next plan
+                StackPlan next = std::move(sc->alts.front());
+                sc->alts.erase(sc->alts.begin());
+                use_plan(sc, std::move(next));
+                sc->tile = sched_default_tile(sc->prog);
+                drop_sched_devices(sc);
+                J.code.clear();
+                continue;
+            }
         }
+        if (!ok) return false;
+        if (const char *d = std::getenv("MK_JIT_DUMP"); d && *d) { // diagnostics: the code object, as loaded,
+            if (FILE *f = std::fopen(d, "wb")) {                   // and its source beside it (<path>.hip)
+                std::fwrite(J.code.data(), 1, J.code.size(), f);
+                std::fclose(f);
+            }
+            if (FILE *f = std::fopen((std::string(d) + ".hip").c_str(), "wb")) {
+                std::fwrite(src.data(), 1, src.size(), f);
+                std::fclose(f);
+            }
+        }
+        break;
     }
+    sc->alts.clear(); // the plan is settled
     J.compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     J.ok = true;
     return true;
@@ -3954,6 +4123,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
             const uint64_t blk = (uint64_t)sc->jit.block, fit = h->jit_lim.slot_bytes / ((uint64_t)hbm_slots * 4u);
             s += " chunk=" + std::to_string(std::max<uint64_t>(blk, fit / blk * blk));
         }
+        if (!sc->occ_note.empty()) s += " stack_plans=" + sc->occ_note; // more_waves: what the checks found
         s += " knobs=" + h->jit_lim.key();
         // resident waves per SIMD of the loaded kernel (registers and LDS;
         // the first device it is loaded on): the occupancy its issue rate is
@@ -4008,6 +4178,7 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         uint32_t pool = 0;
         mk::JitLimits L = h->jit_lim; // as jit_compile: the network's LDS budget
         if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
+        if (sc->max_dops) L.max_dops = std::max(L.max_dops, sc->max_dops);
         if (mk::jit_lane_source(sc->prog, L, lane, why, &shape, nullptr, &heavy, false, &pool))
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
                                                                     L, pool));

@@ -119,13 +119,15 @@ def test_heavy_kernel_slot_layouts(gpu, monkeypatch, layout, depth):
 
 
 # Stack slots in LDS (the heavy kernel's wave owns nslots x 64 words) against
-# HBM, and split between them: by default (tune_lds_auto) D=64 in LDS, D=256
-# and D=400 / 480 split (the first 160 / 320 slots in LDS), D=1024 in HBM;
-# MK_JIT_LDS_SLOTS=0 keeps every slot in HBM, 81920 every slot of D=256 in
-# LDS (three waves per CU).  The pipelined POP loops read LDS.
-@pytest.mark.parametrize("lds,depth,shape", [("auto", 64, "lds"), ("0", 64, "heavy"), ("auto", 256, "split"),
-                                             ("0", 256, "heavy"), ("81920", 256, "lds"), ("auto", 400, "split"),
-                                             ("auto", 480, "split")])
+# HBM, and split between them: by default (tune_lds_auto) D=64 in LDS; D=256
+# (241 registers, 16 slots: eight waves per SIMD) and D=300 (two waves) in
+# LDS with most stack entries in registers (more_waves); D=400 / 480 split
+# (the first 160 / 320 slots in LDS), D=1024 in HBM; MK_JIT_LDS_SLOTS=0 keeps
+# every slot in HBM, 81920 every slot of D=256 in LDS (three waves per CU).
+# The pipelined POP loops read LDS.
+@pytest.mark.parametrize("lds,depth,shape", [("auto", 64, "lds"), ("0", 64, "heavy"), ("auto", 256, "lds"),
+                                             ("auto", 300, "lds"), ("0", 256, "heavy"), ("81920", 256, "lds"),
+                                             ("auto", 400, "split"), ("auto", 480, "split")])
 def test_heavy_kernel_slots_in_lds(gpu, monkeypatch, lds, depth, shape):
     if lds != "auto":
         monkeypatch.setenv("MK_JIT_LDS_SLOTS", lds)

@@ -250,8 +250,12 @@ def test_pipeline_stacks_share_slots(monkeypatch):
 def test_lds_occupancy_tunes_register_count(monkeypatch):
     # The loader's policy for heavy networks (mk_exec.hip tune_lds_auto):
     # D=64's 41 slots fit LDS at four waves per CU: kept, 24 registers; D=256
-    # takes 64 registers (193 slots) and four waves with 160 slots in LDS,
-    # the rest in HBM; D=1024 (961 slots at 64 registers) stays in HBM
+    # gets eight waves per SIMD (more_waves): 241 registers leave 16 slots,
+    # all in a 5 KiB LDS share, and the compiled module holds eight waves
+    # (its VGPRs are checked: stack_plans=w8:...); D=300 cannot reach eight
+    # within 256 registers and gets two (80 slots in 20 KiB); D=400 reaches
+    # neither and keeps 64 registers, four waves per CU, 160 of 337 slots in
+    # LDS; D=1024 (961 slots at 64 registers) stays in HBM
     def fields(depth):
         plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode="jit")
         return dict(w.split("=", 1) for w in plan.split() if "=" in w)
@@ -259,7 +263,13 @@ def test_lds_occupancy_tunes_register_count(monkeypatch):
     f = fields(64)
     assert f["shape"] == "stream-heavy-lds" and f["regs"] == "24" and f["slots"] == "41", f
     f = fields(256)
-    assert f["shape"] == "stream-heavy-split" and f["regs"] == "64" and f["slots"] == "193", f
+    assert f["shape"] == "stream-heavy-lds" and f["regs"] == "241" and f["slots"] == "16", f
+    assert f["stack_plans"].startswith("w8:") and "rejected" not in f["stack_plans"], f
+    assert f["waves_per_simd"] == "8" if "waves_per_simd" in f else True
+    f = fields(300)
+    assert f["shape"] == "stream-heavy-lds" and int(f["slots"]) <= 80 and f["stack_plans"].startswith("w2:"), f
+    f = fields(400)
+    assert f["shape"] == "stream-heavy-split" and f["regs"] == "64" and f["slots"] == "337", f
     f = fields(1024)
     assert f["shape"] == "stream-heavy" and f["regs"] == "64" and f["slots"] == "961", f
     # a fixed LDS budget (MK_JIT_LDS_SLOTS): registers for the most waves
