@@ -2946,8 +2946,19 @@ int ensure_jit_device(SchedCache *sc, int d)
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&jd.per_cu, jd.fn, sc->jit.block, 0) != hipSuccess ||
         jd.per_cu < 1)
         jd.per_cu = 1;
-    if (const char *e = std::getenv("MK_JIT_PER_CU"); e && *e) // diagnostics: resident blocks per CU of the grid
-        jd.per_cu = std::max(1, std::min(jd.per_cu, std::atoi(e)));
+    // The occupancy API ignores part of the SGPR cost on ROCm 7.2: resident
+    // waves per SIMD are at most 800 / (ceil(sgpr / 16) * 16 + 16)
+    // (MI355X_MICROARCH.md; 82-96 SGPRs admit 7 where the API says 8).  A
+    // grid sized by the API's answer leaves a tail of blocks that run only
+    // after others finish.
+    if (const int64_t sg = co_meta(sc->jit.code, ".sgpr_count"); sg > 0) {
+        const int per_simd = 800 / ((int)((sg + 15) / 16) * 16 + 16);
+        const int cap = std::max(1, per_simd * 4 / std::max(1, sc->jit.block / 64));
+        jd.per_cu = std::min(jd.per_cu, cap);
+    }
+    if (const char *e = std::getenv("MK_JIT_PER_CU"); e && *e) // diagnostics: blocks per CU of the grid
+        jd.per_cu = std::max(1, std::atoi(e));
+
     if (std::getenv("MK_JIT_SHOW_GRID"))
         fprintf(stderr, "mk: native kernel on device %d: %d blocks of %d per CU\n", d, jd.per_cu, sc->jit.block);
     return MK_OK;
