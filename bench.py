@@ -226,9 +226,9 @@ def measured_traffic(workload):
 def occupancy_cap(waves_per_simd):
     """Measured VALU issue cap at this many resident waves per SIMD: the best
     rate over independent chains of full-rate int ops in
-    profiles/r04n_valu_rates.jsonl (tools/probe/valu_rates.hip, MI355X), at
+    profiles/valu_rates.jsonl (tools/probe/valu_rates.hip, MI355X), at
     the largest measured occupancy not above it.  None without a match."""
-    p = os.path.join(ROOT, "profiles", "r04n_valu_rates.jsonl")
+    p = os.path.join(ROOT, "profiles", "valu_rates.jsonl")
     if not waves_per_simd or not os.path.exists(p):
         return None
     rows = [json.loads(line) for line in open(p) if line.strip()]
@@ -240,7 +240,7 @@ def occupancy_cap(waves_per_simd):
     best = max((r for r in rows if r["waves_per_simd"] == w), key=lambda r: r["T_lane_ops"])
     return {"waves_per_simd": waves_per_simd, "measured_at_waves_per_simd": w, "cap": best["T_lane_ops"],
             "unit": "Tlane-op/s", "op": best["op"], "chains": best["chains"],
-            "source": "profiles/r04n_valu_rates.jsonl"}
+            "source": "profiles/valu_rates.jsonl"}
 
 
 def valu_peak(stream):
@@ -745,13 +745,28 @@ def main():
     headline = max(bounds, key=lambda b: b["frac"])
     # What the node-instr/s figure is a count of: the
     # executed VALU lane-ops per retired node-instruction from the matching
-    # PMC profile.  Well below 1, the compiler folded the program (C2, C3:
-    # two adds per lane; C4 d64: pushes forwarded to pops in registers) and
-    # node-instr/s counts the reference's work, not issued work: the bound
-    # is then the byte stream, reported as `roofline`.
+    # PMC profile, and whether the compiler folded the program, so that
+    # node-instr/s counts the reference's work rather than issued work.
+    # Folded: a stack network whose PUSH/POPs mostly never reach a slot (C4
+    # d64, d256: pushes forwarded to pops in registers), or a network whose
+    # superblock graph is acyclic (the stream shapes: every lane runs a path
+    # fixed at compile time, C2 and C3 a few adds and branches, whatever
+    # their retired count).  Not folded: the machine shape's loops retire
+    # each iteration (C5); C4 d1024 moves 0.94 slot operations per PUSH/POP.
     vpi = prof.get("valu_lane_ops_per_instr") if sq.get("SQ_INSTS_VALU") else None
+    spp = stack.get("stack_ops_executed_per_push_pop") if stack else None
+    m = re.search(r"\bshape=(\S+)", plan) if "tier=native" in plan else None
+    if spp is not None:
+        folded, basis = spp < 0.5, f"{spp:.3f} stack-slot operations executed per PUSH/POP (folded below 0.5)"
+    elif m:
+        folded = m.group(1).startswith("stream")
+        basis = f"shape={m.group(1)}: " + ("acyclic superblock graph, a path fixed at compile time" if folded
+                                           else "loops that retire each iteration")
+    else:
+        folded, basis = None, "no stack counters and no native module"
     executed = {"valu_lane_ops_per_node_instr": vpi,
-                "compile_folded": None if vpi is None else bool(vpi < 1.0 and headline["bound"] != "valu"),
+                "compile_folded": folded,
+                "folded_basis": basis,
                 "bound": headline["bound"],
                 "note": "node-instr/s counts retired reference instructions; executed VALU lane-ops per "
                         "node-instruction from the PMC profile of this module (null: no matching profile)"}

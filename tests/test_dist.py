@@ -182,3 +182,21 @@ def test_split_covers_batch():
             parts = [mk.dist.split(total, world, r) for r in range(world)]
             assert parts[0][0] == 0 and parts[-1][1] == total
             assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+
+
+def test_bench_reads_only_shipped_profiles():
+    """bench.py's occupancy cap reads profiles/valu_rates.jsonl on the GPU
+    box; a .gpurunignore pattern that matched it would silently null the
+    line's `roofline_issue.occupancy` (round 5: r04n_* matched ./profiles/r0*)."""
+    import fnmatch
+
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pats = [ln.strip() for ln in open(os.path.join(root, ".gpurunignore")) if ln.strip()]
+    for rel in ("profiles/valu_rates.jsonl",):
+        assert os.path.exists(os.path.join(root, rel))
+        for p in pats:
+            assert not fnmatch.fnmatch("./" + rel, p) and not fnmatch.fnmatch(rel, p.lstrip("./")), (rel, p)
+    occ = bench.occupancy_cap(6)
+    assert occ["measured_at_waves_per_simd"] == 4 and occ["cap"] > 40
+    assert bench.occupancy_cap(1)["cap"] < 30 and bench.occupancy_cap(0) is None
