@@ -260,39 +260,70 @@ def sessions_leg(net, n, calls, stream):
     """Stateful mode (row f2) at scale: n independent instances of the
     network, each keeping its node state between calls (program.go:80-92),
     `calls` sequential /compute calls per instance (mk_session_compute_device
-    per call, inputs and results in HBM, one result buffer per call), timed by
-    the host clock around the calls and a final synchronize.  The session
-    kernel is the interpreter's round structure with the instances' state
-    loaded from and stored back to HBM around each call."""
+    per call, inputs and results in HBM, one result buffer per call), timed
+    with HIP events on the sessions' stream around `reps` back-to-back passes
+    (the host clock around the same passes and a final synchronize is
+    reported beside it).  The session kernel is the interpreter's round
+    structure with the instances' state loaded from and stored back to HBM
+    around each call."""
     sess = net.sessions(n)
+    # a stream of its own: a session call given the null stream runs on the
+    # session's own stream (mk.h), which events on the null stream would not
+    # bracket
+    stream = torch.cuda.Stream()
     sh = stream.cuda_stream
     x32 = torch.empty(calls * n, dtype=torch.int32, device="cuda")
     mk.generate_inputs_device(calls * n, x32.data_ptr(), seed=SEED, stream=sh)
+    torch.cuda.synchronize()
     x = x32.to(torch.int64).view(calls, n)  # call c of instance i takes x[c, i]
+    torch.cuda.synchronize()
 
-    def run(burst):
+    def run(burst, reps=0):
+        """From the reset state: one pass (its results are returned), then,
+        with reps > 0, `reps` more passes back to back, the instances keeping
+        their state as sessions do, timed as one span (HIP events on the
+        stream; the host clock beside them).  A single pass between two events
+        is not timed (one launch between two events is mostly launch
+        latency)."""
         out = torch.empty((calls, n), dtype=torch.int32, device="cuda")
         st = torch.empty((calls, n), dtype=torch.uint8, device="cuda")
         sp = torch.empty((calls, n), dtype=torch.int32, device="cuda")
+
+        def one():
+            if burst:  # one launch: every instance's `calls` sequential calls
+                sess.compute_seq_device(x.data_ptr(), calls, out.data_ptr(), st.data_ptr(), sp.data_ptr(), stream=sh)
+            else:
+                for c in range(calls):
+                    sess.compute_device(x[c].data_ptr(), out[c].data_ptr(), st[c].data_ptr(), sp[c].data_ptr(),
+                                        stream=sh)
+
         sess.reset()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if burst:  # one launch: every instance's `calls` sequential calls
-            sess.compute_seq_device(x.data_ptr(), calls, out.data_ptr(), st.data_ptr(), sp.data_ptr(), stream=sh)
-        else:
-            for c in range(calls):
-                sess.compute_device(x[c].data_ptr(), out[c].data_ptr(), st[c].data_ptr(), sp[c].data_ptr(), stream=sh)
+        one()
         torch.cuda.synchronize()
-        secs = time.perf_counter() - t0
+        with torch.cuda.stream(stream):
+            res = (out.clone(), st.clone(), sp.clone())
+        torch.cuda.synchronize()
+        if not reps:
+            return res, None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(reps):
+            one()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        host = (time.perf_counter() - t0) / reps
+        secs = e0.elapsed_time(e1) * 1e-3 / reps
         outs = int(((st & 0x10) != 0).sum())
         total = int(sp.to(torch.int64).sum())
-        return (out, st, sp), {"results_per_s": outs / secs, "node_instr_per_s": total / secs,
-                               "ms_per_call": secs / calls * 1e3}
+        return res, {"results_per_s": outs / secs, "node_instr_per_s": total / secs,
+                     "ms_per_call": secs / calls * 1e3, "host_ms_per_call": host / calls * 1e3, "reps": reps}
 
     run(False)  # warm-up (module load)
     run(True)
-    a, per_call = run(False)
-    b, burst = run(True)
+    a, per_call = run(False, reps=10)
+    b, burst = run(True, reps=10)
     same = all(torch.equal(u, v) for u, v in zip(a, b))
     plan = sess.plan()
     sess.close()
@@ -301,17 +332,18 @@ def sessions_leg(net, n, calls, stream):
     # (superblock 4 B + 8 B per live register, mk_session_plan's state_regs),
     # per call the int64 input, int32 out, u8 status and u32 steps
     # (program.go:80-92: state kept across calls; master.go:216-219).  The
-    # time is the whole launch's (host clock, both kernels), so `frac` is a
-    # lower bound on mk_sess_exec's own (tools/sess_roofline.py has the
-    # rocprofv3 split, profiles/r04o_sessions_roofline.json).
+    # time is the whole launch's (HIP events on the stream, every kernel of
+    # the call), so `frac` is a lower bound on mk_sess_exec's own
+    # (tools/sess_roofline.py has the rocprofv3 split,
+    # profiles/r04o_sessions_roofline.json).
     m = re.search(r"state_regs=(\d+)", plan)
     roof = None
     if m:
         state_b, call_b = 2 * (4 + 8 * int(m.group(1))), 8 + 4 + 1 + 4
         roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK / 1e9,
                 "bytes_per_instance": {"state": state_b, "per_call": call_b},
-                "model": "n x (state + calls x per_call) bytes per launch / launch time (host clock, "
-                         "mk_sess_exec + tis_session)"}
+                "model": "n x (state + calls x per_call) bytes per launch / launch time (HIP events on the "
+                         "sessions' stream around back-to-back launches; every kernel of the call)"}
         for key, res, k in (("burst", burst, calls), ("per_call", per_call, 1)):
             t = res["ms_per_call"] * 1e-3 * k  # one launch
             b = n * (state_b + k * call_b)
@@ -321,7 +353,8 @@ def sessions_leg(net, n, calls, stream):
             "burst_equals_per_call": same, "plan": plan,
             "note": "stateful sessions, inputs resident in HBM: the burst (mk_session_compute_seq_device, "
                     f"{calls} sequential calls per instance in one launch) is the headline; per_call = one "
-                    "mk_session_compute_device launch per call; host clock around the calls; not the value"}
+                    "mk_session_compute_device launch per call; HIP events around the calls (host clock in "
+                    "host_ms_per_call); not the value"}
 
 
 def http_leg(nodes, clients, seconds=5.0):

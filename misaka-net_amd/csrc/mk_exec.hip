@@ -3245,7 +3245,8 @@ struct mk_session {
     // failed leaves handed-off sessions that no kernel will serve again:
     // every call then fails (MK_EDEVICE) until mk_session_reset.
     bool broken = false;
-    hipEvent_t order = nullptr; // orders caller streams against the session's stream
+    hipEvent_t order = nullptr; // recorded after each launch on a caller stream (session_order)
+    hipStream_t last = nullptr; // the stream `order` was last recorded on
     int64_t *regs = nullptr;
     int32_t *slots = nullptr;
     mk::SessMapHdr *hdr = nullptr;
@@ -3665,11 +3666,37 @@ int mk_session_create(mk_net *h, int device, size_t n, const mk_opts *opts, mk_s
     return MK_OK;
 }
 
+namespace mk {
+// Orders work about to be queued on `to` after the session's last launch on
+// a caller stream: a device-side wait on the event recorded after that
+// launch, skipped when `to` is that same stream (stream order already holds;
+// the two-way event hand-off per call had cost ~20 us of stream latency per
+// launch, profiles/r06s_sessions_stream_order.txt).
+int session_wait_last(mk_session *s, hipStream_t to)
+{
+    if (!s->last || s->last == to) return MK_OK;
+    if (hipStreamWaitEvent(to, s->order, 0) != hipSuccess) return MK_EDEVICE;
+    if (to == s->stream) s->last = nullptr; // s->stream now follows every launch so far
+    return MK_OK;
+}
+
+// After a launch on `st` (a caller's or the session's own stream): work queued
+// later on any other stream waits on this.
+int session_mark(mk_session *s, hipStream_t st)
+{
+    if (!s->order && hipEventCreateWithFlags(&s->order, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
+    if (hipEventRecord(s->order, st) != hipSuccess) return MK_EDEVICE;
+    s->last = st;
+    return MK_OK;
+}
+} // namespace mk
+
 int mk_session_reset(mk_session *s)
 {
     if (!s) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
+    if (int rc = mk::session_wait_last(s, s->stream)) return rc;
     if (hipMemsetAsync(s->d_state, 0, s->state_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
     if (s->native && hipMemsetAsync(s->d_native, 0, s->native_bytes, s->stream) != hipSuccess) return MK_EDEVICE;
     if (hipStreamSynchronize(s->stream) != hipSuccess) return MK_EDEVICE;
@@ -3685,20 +3712,14 @@ int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t nca
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    // the session state is ordered on the session's own stream: a caller
-    // stream waits for it (device-side, no host synchronisation), and it for
-    // the caller stream's launches
-    if (stream) {
-        if (!s->order && hipEventCreateWithFlags(&s->order, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
-        if (hipEventRecord(s->order, s->stream) != hipSuccess || hipStreamWaitEvent(st, s->order, 0) != hipSuccess)
-            return MK_EDEVICE;
-    }
+    // the session state is ordered across streams device-side, with no host
+    // synchronisation: this launch after the previous one (a wait only when
+    // that ran on another stream), and the session's own stream's later work
+    // (reset, host calls) after this one
+    if (int rc = mk::session_wait_last(s, st)) return rc;
     int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls);
     if (rc) return rc;
-    if (stream &&
-        (hipEventRecord(s->order, st) != hipSuccess || hipStreamWaitEvent(s->stream, s->order, 0) != hipSuccess))
-        return MK_EDEVICE;
-    return MK_OK;
+    return mk::session_mark(s, st);
 }
 
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
@@ -3743,6 +3764,7 @@ int session_host_calls(mk_session *s, const int64_t *in, size_t ncalls, int32_t 
     if (ncalls > 0xffffffffull) return MK_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
+    if (int rc = mk::session_wait_last(s, s->stream)) return rc;
     const size_t m = s->n * ncalls;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t a8 = al(m * 8), a4 = al(m * 4), need = a8 + a4 + a4 + al(m);
@@ -3788,12 +3810,14 @@ int session_host_calls(mk_session *s, const int64_t *in, size_t ncalls, int32_t 
 template <class T>
 int sget(mk_session *s, const T *dev, T &v)
 {
+    if (int rc = session_wait_last(s, s->stream)) return rc;
     if (hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, s->stream) != hipSuccess) return MK_EDEVICE;
     return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
 }
 template <class T>
 int sput(mk_session *s, T *dev, const T &v)
 {
+    if (int rc = session_wait_last(s, s->stream)) return rc;
     if (hipMemcpyAsync(dev, &v, sizeof(T), hipMemcpyHostToDevice, s->stream) != hipSuccess) return MK_EDEVICE;
     return hipStreamSynchronize(s->stream) == hipSuccess ? MK_OK : MK_EDEVICE;
 }
@@ -3944,6 +3968,7 @@ int mk_session_cancel(mk_session *s)
     if (s->n == 0) return MK_OK;
     std::lock_guard<std::mutex> lk(s->mu);
     mk::DeviceGuard g(s->device);
+    if (int rc = mk::session_wait_last(s, s->stream)) return rc;
     uint32_t *io = s->p.io;
     uint64_t n = s->n;
     void *args[] = {(void *)&io, (void *)&n};

@@ -3,6 +3,8 @@
 # rocprofv3 --pmc pass (kernel trace only) of SQ wave / wait / active-instruction
 # counters, each under its own time limit.
 #   bash tools/gpu_pmc_stall.sh TAG CONFIG [ENV=VALUE ...]
+# PMC_ARGS="script args" profiles `python3 script args` instead of the bench
+# config (CONFIG then only names the output directory).
 set -o pipefail
 TAG=$1; CFG=$2; shift 2
 OUT=gpurun_out/$TAG/$CFG
@@ -15,7 +17,7 @@ STALL2="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_
 for pass in STALL STALL2; do
 echo "[pmc-stall] $(date +%T) $CFG $pass"
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc ${!pass} --output-format csv -d "$OUT/$pass" -o p -- \
-  python3 bench.py --config $CFG --steps 6 --warmup 1 --no-cpu-baseline > "$OUT/$pass.log" 2>&1 \
+  python3 ${PMC_ARGS:-bench.py --config $CFG --steps 6 --warmup 1 --no-cpu-baseline} > "$OUT/$pass.log" 2>&1 \
   || { echo "[pmc-stall] failed"; tail -5 "$OUT/$pass.log"; exit 1; }
 python3 - "$OUT/$pass" <<'PY'
 import collections, csv, glob, sys
