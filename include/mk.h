@@ -203,9 +203,10 @@ int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int3
                            uint32_t *steps);
 
 /* One call on device arrays, asynchronous on `stream` (NULL = the session's
- * own stream); calls on one session are ordered (device-side: a caller stream
- * and the session's stream wait for each other through an event, no host
- * synchronisation). */
+ * own stream); calls on one session are ordered device-side, with no host
+ * synchronisation: a call waits on an event recorded after the previous
+ * launch when that ran on another stream (calls on one stream follow stream
+ * order), and the session's synchronous calls below wait on it too. */
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
                               uint32_t *d_steps, void *stream);
 
