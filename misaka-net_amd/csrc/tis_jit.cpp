@@ -87,6 +87,7 @@ struct Graph {
     std::vector<char> narrow;    // register whose high 32 bits nothing reads (narrow_regs): uint32_t
     size_t nreach = 0, ndops = 0; // ndops: micro-ops emitted (rolled runs count once)
     bool cyclic = false;
+    std::vector<std::vector<uint32_t>> succ; // per reachable variant, its exits' targets
     std::vector<std::vector<Run>> runs; // per variant, ascending start
     const JitLimits *lim = nullptr;
 };
@@ -325,7 +326,38 @@ bool analyze(const SchedProgram &p, const JitLimits &lim, Graph &g, std::string 
             st.pop_back();
         }
     }
+    g.succ = std::move(succ);
     return true;
+}
+
+// The reachable variants in reverse postorder from variant 0: every edge
+// goes forward except the back edges of cycles (a JRO's backward arms, a
+// lane's wrap to its program's start) and self-loops.
+std::vector<uint32_t> forward_order(const Graph &g)
+{
+    const size_t nv = g.entry.size();
+    std::vector<std::vector<uint32_t>> succ = g.succ;
+    for (auto &l : succ) std::sort(l.begin(), l.end(), std::greater<uint32_t>());
+    std::vector<uint8_t> col(nv, 0);
+    std::vector<uint32_t> post;
+    std::vector<std::pair<uint32_t, size_t>> st{{0u, 0}};
+    col[0] = 1;
+    while (!st.empty()) {
+        auto &[v, k] = st.back();
+        if (k < succ[v].size()) {
+            // successors in descending id order, so that the lower ids (a
+            // fast variant before its checked one) come first in the result
+            const uint32_t w = succ[v][k++];
+            if (!col[w]) {
+                col[w] = 1;
+                st.push_back({w, 0});
+            }
+        } else {
+            post.push_back(v);
+            st.pop_back();
+        }
+    }
+    return std::vector<uint32_t>(post.rbegin(), post.rend());
 }
 
 // Registers whose high 32 bits no reachable op ever reads.  ACC and BAK are
@@ -1700,6 +1732,20 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("}");
     e.s.insert(fn_start, tab.s);
     e.line("// %zu self-loops", loops.size());
+    // the sweep dispatcher's order (JitLimits::sweep, kMachineSortKernel):
+    // one pass over the variants in forward order runs every lane as far as
+    // the graph's forward edges take it
+    if (g.lim->sweep && !p.session) {
+        const std::vector<uint32_t> fo = forward_order(g);
+        {
+            std::string l = "#define MK_SWEEP_LIST(X)";
+            for (uint32_t v : fo) {
+                size_t gpc = 0, xpc = 0;
+                l += " X(" + std::to_string(v) + "u, " + (self_loop(g, v, gpc, xpc) ? "1" : "0") + ")";
+            }
+            e.s += l + "\n";
+        }
+    }
     e.line("MK_FN bool mk_is_loop(const uint32_t u)");
     e.line("{");
     if (loops.empty()) {
@@ -2161,6 +2207,20 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             MkLane L;
             mk_init(L, live ? s_key[j] : 0);
             if (!live) L.sb = MK_SB_IDLE;
+#if defined(MK_SWEEP_LIST)
+            // sweep dispatch (MK_JIT_SWEEP): the variants in forward order,
+            // each run for the lanes on it, skipped by one ballot when none
+            // is; lanes a loop left behind go round again
+#define MK_SWEEP_STEP(v, loop)                                                                   \
+            if (__ballot(L.sb == (v))) {                                                             \
+                const uint32_t smax_ = (loop) ? MK_WAVE_MAX(L.sb == (v) ? L.steps : 0u) : 0u;        \
+                if (L.sb == (v)) mk_run((v), L, p.budget, slots, p.lanes, pol, smax_);               \
+            }
+            while (__ballot(L.sb < MK_SB_DONE)) {
+                MK_SWEEP_LIST(MK_SWEEP_STEP)
+            }
+#undef MK_SWEEP_STEP
+#else
             for (;;) {
                 const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
                 if (!actb) break;
@@ -2178,6 +2238,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
                 ++pf_rounds;
 #endif
             }
+#endif
             if (live) {
                 const uint32_t at = s_pos[j];
                 s_out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
@@ -2292,6 +2353,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_SAT_BLOCK", l.sat_block);
     if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
     flag("MK_JIT_TS_DYN", l.ts_dyn);
+    flag("MK_JIT_SWEEP", l.sweep);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
@@ -2318,7 +2380,7 @@ std::string JitLimits::key() const
              (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
     std::string k = b;
     if (!sat_count) k += ",scount=0";
-
+    if (!sweep) k += ",sweep=0";
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
     if (!prio) k += ",prio=0";

@@ -117,6 +117,11 @@ struct JitLimits {
     // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
     // order.
     bool ts_dyn = false;
+    // kMachineSortKernel dispatches by sweeps over the variants in reverse
+    // postorder (tis_jit.cpp forward_order), each variant one ballot when no
+    // lane is on it, instead of one variant per round (MK_JIT_SWEEP=0: rounds;
+    // C5 105.8 -> 97.0 us, profiles/r06u_c5_sweep_ab.txt).
+    bool sweep = true;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
