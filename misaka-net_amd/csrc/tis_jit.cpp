@@ -1734,8 +1734,11 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     e.line("// %zu self-loops", loops.size());
     // the sweep dispatcher's order (JitLimits::sweep, kMachineSortKernel):
     // one pass over the variants in forward order runs every lane as far as
-    // the graph's forward edges take it
-    if (g.lim->sweep && !p.session) {
+    // the graph's forward edges take it.  Machines of few variants keep the
+    // rounds: their compare tree is shallow and a round cheap (jro_heavy, 6
+    // variants: 52.3 ms by rounds, 58.8 by sweeps; C5, 36: 105.8 -> 97.0 us;
+    // two_stacks and dyn_depth unchanged, profiles/r06w_sweep_census_ab.txt)
+    if (g.lim->sweep && !p.session && g.nreach >= kSweepMinVariants) {
         const std::vector<uint32_t> fo = forward_order(g);
         {
             std::string l = "#define MK_SWEEP_LIST(X)";

@@ -229,6 +229,8 @@ constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
 constexpr int kJitHeavyBlock = 64;
+// Machines of at least this many reachable variants dispatch by sweeps (JitLimits::sweep).
+constexpr size_t kSweepMinVariants = 16;
 constexpr int kJitPoolBlock = 64;         // the pool kernel: one wave per block, its own pool
 constexpr size_t kJitPoolBytes = 12288;   // LDS for one wave's lane pool (slots = bytes / lane state)
 constexpr uint32_t kJitPoolMaxSlots = 256;
