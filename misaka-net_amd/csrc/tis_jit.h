@@ -122,6 +122,8 @@ struct JitLimits {
     // lane is on it, instead of one variant per round (MK_JIT_SWEEP=0: rounds;
     // C5 105.8 -> 97.0 us, profiles/r06u_c5_sweep_ab.txt).
     bool sweep = true;
+    // the sweep's checked variants last, behind one ballot (MK_JIT_SWEEP_COLD=0: in order)
+    bool sweep_cold = true;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
