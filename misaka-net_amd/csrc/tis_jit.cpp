@@ -1738,7 +1738,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // rounds: their compare tree is shallow and a round cheap (jro_heavy, 6
     // variants: 52.3 ms by rounds, 58.8 by sweeps; C5, 36: 105.8 -> 97.0 us;
     // two_stacks and dyn_depth unchanged, profiles/r06w_sweep_census_ab.txt)
-    if (g.lim->sweep && !p.session && g.nreach >= kSweepMinVariants) {
+    if (g.lim->sweep && g.nreach >= kSweepMinVariants) {
         const std::vector<uint32_t> fo = forward_order(g);
         // the checked variants (a budget's last round: rare) go last, behind
         // one ballot over a mask of their ids, when the ids fit one (C5: 18
@@ -2878,6 +2878,23 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
         L.outv = 0;
         L.next = MK_SS_DEAD;
         if (run) mk_sess_input(L, (int64_t)(int32_t)p.in[ci]); // int32(v) at GetInput (master.go:237)
+#if defined(MK_SWEEP_LIST)
+        // sweep dispatch, as kMachineSortKernel's (JitLimits::sweep)
+#define MK_SWEEP_STEP(v, loop)                                                                   \
+        if (__ballot(L.sb == (v))) {                                                                 \
+            const uint32_t smax_ = (loop) ? MK_WAVE_MAX(L.sb == (v) ? L.steps : 0u) : 0u;            \
+            if (L.sb == (v)) mk_run((v), L, p.budget, slots, p.n, MK_POLICY, smax_);                 \
+        }
+        while (__ballot(L.sb < MK_SB_DONE)) {
+            MK_SWEEP_LIST(MK_SWEEP_STEP)
+#if defined(MK_SWEEP_COLD)
+            if (__ballot(L.sb < 64u && ((MK_SWEEP_COLD_MASK >> L.sb) & 1ull))) {
+                MK_SWEEP_COLD(MK_SWEEP_STEP)
+            }
+#endif
+        }
+#undef MK_SWEEP_STEP
+#else
         for (;;) {
             const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
             if (!actb) break;
@@ -2886,6 +2903,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
             const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
             if (L.sb == u) mk_run(us, L, p.budget, slots, p.n, MK_POLICY, smax);
         }
+#endif
         if (!live || sbv == MK_SS_T1 || sbv == MK_SS_HAND) continue; // the interpreter answers these
         if (run && L.st == MK_SS_HANDOFF) {
             p.hand_sb[gid] = L.next / 2u;

@@ -2,7 +2,7 @@
 network, K launches of one kind only, so that the kernel statistics and the
 PMC passes describe that kind of launch alone.
 
-    python tools/probe/session_prof.py percall|burst [n] [K] [calls]
+    python tools/probe/session_prof.py percall|burst [n] [K] [calls] [network]
 
 percall: K launches of mk_session_compute_device (one call per instance per
 launch); burst: K launches of mk_session_compute_seq_device with `calls`
@@ -23,11 +23,14 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 calls = int(sys.argv[4]) if len(sys.argv) > 4 else 8
 torch.cuda.init()
-net = mk.Network(mk.networks.example_network())
+net_name = sys.argv[5] if len(sys.argv) > 5 else "example"
+net = mk.Network(getattr(mk.networks, net_name + "_network")())
 sess = net.sessions(n)
 sh = torch.cuda.current_stream().cuda_stream
 x32 = torch.empty(calls * n, dtype=torch.int32, device="cuda")
 mk.generate_inputs_device(calls * n, x32.data_ptr(), seed=0x4D49534B41, stream=sh)
+if net_name == "countdown":  # C5's inputs: uniform in [0, 1023]
+    x32 &= 1023
 x = x32.to(torch.int64).view(calls, n)
 out = torch.empty((calls, n), dtype=torch.int32, device="cuda")
 st = torch.empty((calls, n), dtype=torch.uint8, device="cuda")
