@@ -3255,6 +3255,7 @@ struct mk_session {
     ~mk_session()
     {
         mk::DeviceGuard g(device);
+        if (last && order) (void)hipEventSynchronize(order); // the last launch on a caller stream
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipFree(d_state);
         (void)hipFree(d_native);
