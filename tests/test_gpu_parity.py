@@ -897,6 +897,42 @@ def test_session_device_bursts_match_oracle(gpu, seed):
         g.close()
 
 
+# Consecutive calls of one session set on different streams, with no host
+# synchronisation between the device calls: two caller streams, the null
+# stream (the session's own) and the host API.  Each call needs the state the
+# previous one left, so the library's cross-stream ordering (mk_exec.hip
+# session_wait_last / session_mark) is what keeps the results exact.  C5's
+# countdown network: long kernels, and machine modules dispatching by sweeps.
+def test_session_calls_across_streams_match_oracle(gpu):
+    import torch
+
+    nodes = mk.networks.countdown_network()
+    n, calls = 1 << 15, 7
+    xs = po.gen_inputs(77, calls * n, kind=1, mask=1023).reshape(calls, n)
+    o = po.OracleSessions(po.OracleNet(nodes), n)
+    refs = [o.compute(row, threads=THREADS) for row in xs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    x = torch.from_numpy(xs).cuda()
+    torch.cuda.synchronize()
+    g = mk.Network(nodes).sessions(n)
+    out = torch.empty((calls, n), dtype=torch.int32, device="cuda")
+    st = torch.empty((calls, n), dtype=torch.uint8, device="cuda")
+    sp = torch.empty((calls, n), dtype=torch.int32, device="cuda")
+    host = {}
+    for c, where in enumerate(["s1", "s2", "null", "s1", "host", "s2", "s2"]):
+        if where == "host":
+            host[c] = g.compute(xs[c])
+            continue
+        stream = {"s1": s1.cuda_stream, "s2": s2.cuda_stream, "null": None}[where]
+        g.compute_device(x[c].data_ptr(), out[c].data_ptr(), st[c].data_ptr(), sp[c].data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    for c in range(calls):
+        got = host[c] if c in host else mk.network.BatchResult(out[c].cpu().numpy(), st[c].cpu().numpy(),
+                                                               sp[c].cpu().numpy().astype(np.uint32))
+        assert_same(got, refs[c], f"call {c}")
+    g.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fill", ["zeros", "sevens", "halves"])
 def test_machine_tiles_of_equal_inputs(gpu, fill):
