@@ -15,8 +15,10 @@
 //   machine -- the graph has cycles (loops whose trip counts follow the
 //              data): each thread holds one lane as a small state machine
 //              (superblock id + registers), a wave-uniform dispatcher runs
-//              one superblock at a time for the lanes sitting on it, and a
-//              lane that ends takes its next input while the others go on.
+//              one superblock at a time for the lanes sitting on it (rounds),
+//              or every superblock in turn in forward order (sweeps, machines
+//              of kSweepMinVariants or more), and a lane that ends takes its
+//              next input while the others go on.
 #include "tis_jit.h"
 
 #include <algorithm>
