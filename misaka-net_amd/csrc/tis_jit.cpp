@@ -1739,8 +1739,13 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // the graph's forward edges take it.  Machines of few variants keep the
     // rounds: their compare tree is shallow and a round cheap (jro_heavy, 6
     // variants: 52.3 ms by rounds, 58.8 by sweeps; C5, 36: 105.8 -> 97.0 us;
-    // two_stacks and dyn_depth unchanged, profiles/r06w_sweep_census_ab.txt)
-    if (g.lim->sweep && g.nreach >= kSweepMinVariants) {
+    // two_stacks and dyn_depth unchanged, profiles/r06w_sweep_census_ab.txt).
+    // The kernel runs MK_SWEEP_PASSES passes, then rounds for the lanes left
+    // (loops over several variants: each iteration would cost a whole pass),
+    // and machines of very many variants keep the rounds (a 190-variant test
+    // network: 220 ms by rounds, 403 ms with one pass first, 1,348 ms by
+    // sweeps alone; profiles/r07l_sweep_random_ab.txt)
+    if (g.lim->sweep && g.nreach >= kSweepMinVariants && g.nreach <= kSweepMaxVariants) {
         const std::vector<uint32_t> fo = forward_order(g);
         // the checked variants (a budget's last round: rare) go last, behind
         // one ballot over a mask of their ids, when the ids fit one (C5: 18
@@ -2231,13 +2236,13 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 #if defined(MK_SWEEP_LIST)
             // sweep dispatch (MK_JIT_SWEEP): the variants in forward order,
             // each run for the lanes on it, skipped by one ballot when none
-            // is; lanes a loop left behind go round again
+            // is; MK_SWEEP_PASSES passes, then the rounds below
 #define MK_SWEEP_STEP(v, loop)                                                                   \
             if (__ballot(L.sb == (v))) {                                                             \
                 const uint32_t smax_ = (loop) ? MK_WAVE_MAX(L.sb == (v) ? L.steps : 0u) : 0u;        \
                 if (L.sb == (v)) mk_run((v), L, p.budget, slots, p.lanes, pol, smax_);               \
             }
-            while (__ballot(L.sb < MK_SB_DONE)) {
+            for (uint32_t ps = 0; ps < MK_SWEEP_PASSES && __ballot(L.sb < MK_SB_DONE); ++ps) {
                 MK_SWEEP_LIST(MK_SWEEP_STEP)
 #if defined(MK_SWEEP_COLD)
                 if (__ballot(L.sb < 64u && ((MK_SWEEP_COLD_MASK >> L.sb) & 1ull))) {
@@ -2246,7 +2251,9 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 #endif
             }
 #undef MK_SWEEP_STEP
-#else
+#endif
+            // rounds: the lowest lane's variant at a time (after the sweep
+            // passes, for the lanes they left: loops over several variants)
             for (;;) {
                 const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
                 if (!actb) break;
@@ -2264,7 +2271,6 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
                 ++pf_rounds;
 #endif
             }
-#endif
             if (live) {
                 const uint32_t at = s_pos[j];
                 s_out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
@@ -2381,6 +2387,7 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TS_DYN", l.ts_dyn);
     flag("MK_JIT_SWEEP", l.sweep);
     flag("MK_JIT_SWEEP_COLD", l.sweep_cold);
+    num("MK_JIT_SWEEP_PASSES", l.sweep_passes);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
@@ -2409,6 +2416,7 @@ std::string JitLimits::key() const
     if (!sat_count) k += ",scount=0";
     if (!sweep) k += ",sweep=0";
     if (!sweep_cold) k += ",scold=0";
+    if (sweep_passes != 1) k += ",spass=" + std::to_string(sweep_passes);
     if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
     if (!prio) k += ",prio=0";
@@ -2741,6 +2749,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
+    e.line("#define MK_SWEEP_PASSES %uu", lim.sweep_passes); // kMachineSortKernel: sweep passes before rounds
     if (lim.prof) { // kMachineSortKernel: cycles per phase in place of the counters (MK_JIT_PROF)
         e.line("#define MK_PROF 1");
         e.line("#define MK_T() __builtin_amdgcn_s_memtime()");
@@ -2887,7 +2896,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
             const uint32_t smax_ = (loop) ? MK_WAVE_MAX(L.sb == (v) ? L.steps : 0u) : 0u;            \
             if (L.sb == (v)) mk_run((v), L, p.budget, slots, p.n, MK_POLICY, smax_);                 \
         }
-        while (__ballot(L.sb < MK_SB_DONE)) {
+        for (uint32_t ps = 0; ps < MK_SWEEP_PASSES && __ballot(L.sb < MK_SB_DONE); ++ps) {
             MK_SWEEP_LIST(MK_SWEEP_STEP)
 #if defined(MK_SWEEP_COLD)
             if (__ballot(L.sb < 64u && ((MK_SWEEP_COLD_MASK >> L.sb) & 1ull))) {
@@ -2896,8 +2905,8 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
 #endif
         }
 #undef MK_SWEEP_STEP
-#else
-        for (;;) {
+#endif
+        for (;;) { // rounds, for the lanes the sweep passes left
             const unsigned long long actb = __ballot(L.sb < MK_SB_DONE);
             if (!actb) break;
             const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)L.sb, (int)__builtin_ctzll(actb));
@@ -2905,7 +2914,6 @@ extern "C" __global__ void __launch_bounds__(256) mk_sess_exec(SessK p)
             const uint32_t us = MK_SCALAR(u); // the switch value, out of GVN's reach (MK_JIT_UNIFORM_SW)
             if (L.sb == u) mk_run(us, L, p.budget, slots, p.n, MK_POLICY, smax);
         }
-#endif
         if (!live || sbv == MK_SS_T1 || sbv == MK_SS_HAND) continue; // the interpreter answers these
         if (run && L.st == MK_SS_HANDOFF) {
             p.hand_sb[gid] = L.next / 2u;

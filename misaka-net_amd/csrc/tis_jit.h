@@ -124,6 +124,8 @@ struct JitLimits {
     bool sweep = true;
     // the sweep's checked variants last, behind one ballot (MK_JIT_SWEEP_COLD=0: in order)
     bool sweep_cold = true;
+    // sweep passes before the round dispatcher takes the lanes left (MK_JIT_SWEEP_PASSES)
+    uint32_t sweep_passes = 1;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
@@ -231,8 +233,9 @@ constexpr const char *kJitKernel = "mk_jit_exec";
 constexpr int kJitBlock = 256;
 constexpr int kJitStreamLanes = 4; // lanes per thread per tile (stream shape)
 constexpr int kJitHeavyBlock = 64;
-// Machines of at least this many reachable variants dispatch by sweeps (JitLimits::sweep).
-constexpr size_t kSweepMinVariants = 16;
+// Machines of kSweepMinVariants to kSweepMaxVariants reachable variants
+// dispatch by sweeps first (JitLimits::sweep).
+constexpr size_t kSweepMinVariants = 16, kSweepMaxVariants = 128;
 constexpr int kJitPoolBlock = 64;         // the pool kernel: one wave per block, its own pool
 constexpr size_t kJitPoolBytes = 12288;   // LDS for one wave's lane pool (slots = bytes / lane state)
 constexpr uint32_t kJitPoolMaxSlots = 256;
