@@ -2749,7 +2749,8 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
-    e.line("#define MK_SWEEP_PASSES %uu", lim.sweep_passes); // kMachineSortKernel: sweep passes before rounds
+    if (shape == JIT_MACHINE) // machine kernels: sweep passes before rounds (stream modules' sources as they were)
+        e.line("#define MK_SWEEP_PASSES %uu", lim.sweep_passes);
     if (lim.prof) { // kMachineSortKernel: cycles per phase in place of the counters (MK_JIT_PROF)
         e.line("#define MK_PROF 1");
         e.line("#define MK_T() __builtin_amdgcn_s_memtime()");
