@@ -226,14 +226,17 @@ def measured_traffic(workload):
 def occupancy_cap(waves_per_simd):
     """Measured VALU issue cap at this many resident waves per SIMD: the best
     rate over independent chains of full-rate int ops in
-    profiles/valu_rates.jsonl (tools/probe/valu_rates.hip, MI355X), at
-    the largest measured occupancy not above it.  None without a match."""
+    profiles/valu_rates.jsonl (tools/probe/valu_rates.hip, MI355X; rows for
+    every occupancy 1..8 since round 6).  A fractional occupancy (15 one-wave
+    blocks per CU are 3.75 per SIMD) is priced at its whole part, explicitly:
+    `measured_at_waves_per_simd`.  None without a match."""
     p = os.path.join(ROOT, "profiles", "valu_rates.jsonl")
     if not waves_per_simd or not os.path.exists(p):
         return None
     rows = [json.loads(line) for line in open(p) if line.strip()]
     rows = [r for r in rows if r["op"] in ("add_u32_vop2", "sub_clamp_vop3")]
-    ws = [r["waves_per_simd"] for r in rows if r["waves_per_simd"] <= waves_per_simd]
+    whole = int(waves_per_simd)
+    ws = [r["waves_per_simd"] for r in rows if r["waves_per_simd"] <= whole]
     if not ws:
         return None
     w = max(ws)
@@ -583,11 +586,23 @@ def main():
     # `value`, which stays the sharded compute (no data-path collective).
     e2e = None
     if dist and (world > 1 or args.gather):
-        e2e_s, g_out, g_st = mk.dist.timed_gather(lambda: step(False), out, st, dist, args.steps,
-                                                  sync=torch.cuda.synchronize)
+        # each step's outputs and statuses in one packed buffer (one gather
+        # per step), two buffers so that step k's gather overlaps step k + 1
+        packs = [torch.empty(5 * lanes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        pack_run = []
+        for pk in packs:
+            o_v, s_v = mk.dist.pack_views(pk, lanes)
+            pack_run.append(net.device_launcher(lanes, out_ptr=o_v.data_ptr(), status_ptr=s_v.data_ptr(),
+                                                in_ptr=None if args.gen_inputs else x.data_ptr(),
+                                                in_kind=N.MK_IN_I32, seed=SEED, gen_kind=gen_kind,
+                                                gen_mask=mask, offset=lo, device=dev, mode=args.mode))
+        e2e_s, g = mk.dist.timed_gather(lambda b: pack_run[b](sh), packs, dist, args.steps,
+                                        sync=torch.cuda.synchronize)
+        g_out, g_st = mk.dist.unpack_gathered(g, lanes, world) if rank == 0 else (None, None)
         e2e = {"value": None, "ms_per_step": e2e_s / args.steps * 1e3,
-               "gathered_bytes_per_step": 5 * lanes * world, "collective": "ordered gather to rank 0 "
-               f"({dist.get_backend()}), outputs int32 + status u8"}
+               "gathered_bytes_per_step": 5 * lanes * world, "collectives_per_step": 1,
+               "collective": f"ordered gather to rank 0 ({dist.get_backend()}) of one packed buffer per rank "
+               "(outputs int32 + status u8), issued async so that it overlaps the next step"}
         if args.verify_gather and rank == 0:
             # the gathered shards == one launch over all world x lanes global lanes
             def full():
@@ -707,8 +722,8 @@ def main():
         # the same executed rate against what a kernel at this occupancy can
         # issue (one wave per SIMD issues a VALU op only
         # every ~8.8 cycles), reproducible from profiles/
-        m = re.search(r"waves_per_simd=(\d+)", plan)
-        occ = occupancy_cap(int(m.group(1)) if m else 0)
+        m = re.search(r"waves_per_simd=([\d.]+)", plan)
+        occ = occupancy_cap(float(m.group(1)) if m else 0)
         if occ:
             occ["frac"] = issue["achieved"] / occ["cap"]
         issue["occupancy"] = occ

@@ -1563,10 +1563,17 @@ struct SchedCache {
     std::vector<StackPlan> alts; // the next plans to try when that check fails (tune_lds_auto)
     std::string occ_note;     // what the check found (mk_net_plan occupancy=)
     std::string why;
-    SchedProgram prog;
+    SchedProgram prog;  // the schedule the native tier compiles (a more_waves plan, or the default)
+    // Tier 2's schedule while the native tier tries a more_waves plan: the
+    // default plan (its register file lives in LDS, so the plans' hundreds of
+    // registers would leave tier 2 one 64-lane block per CU).  Null: prog.
+    std::unique_ptr<SchedProgram> t2;
     SchedDev dev[kMaxDevices];
     JitState jit;
 };
+
+// The schedule tier 2 (and the interpreter's superblock-count test) uses.
+const SchedProgram &tier2_prog(const SchedCache *sc) { return sc->t2 ? *sc->t2 : sc->prog; }
 
 struct DevCtx {
     bool ready = false;
@@ -1880,6 +1887,7 @@ std::vector<StackPlan> more_waves(mk_net *h, SchedCache *sc, const SchedLimits &
 // Installs a plan (a tuning choice, or the next after a failed check).
 void use_plan(SchedCache *sc, StackPlan &&sp)
 {
+    if (!sp.waves) sc->t2.reset(); // the default plan: tier 2's own (tier2_prog)
     sc->prog = std::move(sp.prog);
     sc->lds_set = true;
     sc->lds_bytes = sp.lds_bytes;
@@ -1905,7 +1913,21 @@ void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
     const JitLimits &jl = h->jit_lim;
     auto bytes = [&](uint32_t n) { return ((uint64_t)jit_lds_words(n, jl.lds_quad) * 256u + 2047u) / 2048u * 2048u; };
     if (!heavy_stream(sc->prog, jl)) return;
-    if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) return; // the knob's budget holds them
+    if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) {
+        // the knob's budget holds them at four waves per CU (C4 D=64: 41
+        // slots, 15 waves per CU): more waves per SIMD when more registers
+        // shrink the slots to their share (more_waves), else as they are
+        std::vector<StackPlan> more = more_waves(h, sc, lim0, sc->prog.nregs, sc->prog.nslots);
+        if (more.empty()) return;
+        StackPlan def;
+        def.prog = sc->prog;
+        def.lds_bytes = jl.lds_slot_bytes;
+        for (size_t k = 1; k < more.size(); ++k) sc->alts.push_back(std::move(more[k]));
+        sc->t2 = std::make_unique<SchedProgram>(def.prog); // tier 2 keeps the default plan
+        sc->alts.push_back(std::move(def));
+        use_plan(sc, std::move(more[0]));
+        return;
+    }
     SchedProgram best = sc->prog;
     for (uint32_t r = 64u; r > lim0.soft_regs; r -= 8u) {
         SchedLimits l = lim0;
@@ -1936,6 +1958,7 @@ void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
         return;
     }
     for (size_t k = 1; k < more.size(); ++k) sc->alts.push_back(std::move(more[k]));
+    sc->t2 = std::make_unique<SchedProgram>(def.prog); // tier 2 keeps the default plan
     sc->alts.push_back(std::move(def));
     use_plan(sc, std::move(more[0]));
 }
@@ -2070,7 +2093,7 @@ int ensure_sched_device(SchedCache *sc, int d)
     SchedDev &sd = sc->dev[d];
     if (sd.d_code) return MK_OK;
     DeviceGuard g(d);
-    const SchedProgram &P = sc->prog;
+    const SchedProgram &P = tier2_prog(sc);
     sched_geometry(P.nregs, sd.block, sd.slots);
     std::vector<uint32_t> entry;
     const std::vector<DOp> code = assemble_device(P, sd.block * sd.slots * 8, entry);
@@ -2124,7 +2147,7 @@ int launch_sched_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, si
     if (rc) return rc;
     DevCtx &c = h->dev[d];
     SchedDev &sd = sc->dev[d];
-    const SchedProgram &P = sc->prog;
+    const SchedProgram &P = tier2_prog(sc);
     DeviceGuard g(d);
     // LDS register file [nregs][K][B] x 8 B; block size and slot count are
     // fixed by the assembly (sched_geometry).
@@ -2832,9 +2855,10 @@ int64_t co_meta(const std::vector<char> &co, const char *key)
 }
 
 // Whether a module holds `waves` waves per SIMD: VGPRs + AGPRs in 8-register
-// granules within gfx950's 512 per SIMD lane, and no scratch.  `note` says
-// what was found.
-bool module_holds(const std::vector<char> &co, uint32_t waves, std::string &note)
+// granules within gfx950's 512 per SIMD lane (`vgpr_file`:
+// JitLimits::vgpr_file, lowered only by the tests that take the fallback
+// path), and no scratch.  `note` says what was found.
+bool module_holds(const std::vector<char> &co, uint32_t waves, uint32_t vgpr_file, std::string &note)
 {
     const int64_t v = co_meta(co, ".vgpr_count"), a = co_meta(co, ".agpr_count"),
                   ps = co_meta(co, ".private_segment_fixed_size");
@@ -2842,26 +2866,7 @@ bool module_holds(const std::vector<char> &co, uint32_t waves, std::string &note
     char b[96];
     snprintf(b, sizeof b, "w%u:v%lld,a%lld,s%lld", waves, (long long)v, (long long)a, (long long)ps);
     note = b;
-    return v >= 0 && ps == 0 && alloc * (int64_t)waves <= 512;
-}
-
-// Drops a SchedCache's tier-2 device code and slots (after its schedule
-// changed; rebuilt on next use).  Caller holds h->mu.
-void drop_sched_devices(SchedCache *sc)
-{
-    for (int d = 0; d < kMaxDevices; d++) {
-        SchedDev &sd = sc->dev[d];
-        if (!sd.d_code && !sd.d_slots && !sd.d_order) continue;
-        DeviceGuard g(d);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(sd.d_code);
-        (void)hipFree(sd.d_entry);
-        (void)hipFree(sd.d_jtab);
-        (void)hipFree(sd.d_slots);
-        (void)hipFree(sd.d_order);
-        (void)hipFree(sd.d_ordtab);
-        sd = SchedDev{};
-    }
+    return v >= 0 && ps == 0 && alloc * (int64_t)waves <= (int64_t)vgpr_file;
 }
 
 // Caller holds h->mu.  Generates and compiles once per SchedCache (hiprtc,
@@ -2885,6 +2890,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
         return false;
     }
     const auto t0 = std::chrono::steady_clock::now();
+    int compiles = 0;
     for (;;) {
         JitLimits L = lim; // the network's LDS budget, when the loader chose one (tune_lds_auto)
         if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
@@ -2900,10 +2906,22 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
             src = jit_module_source(lane, J.shape, J.heavy, L, J.pool);
             J.src_bytes = src.size();
             J.src_hash = src_hash(src);
-            ok = rtc_compile(src, lim.max_compile_s, J.code, J.why, J.rtc);
+            // one wall-clock bound for all the plans' compiles together (the
+            // first compile gets at least a tenth of it; a later plan none
+            // when it is spent, and the network stays on tier 2)
+            const double left = lim.max_compile_s -
+                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (compiles && left <= 0.0) {
+                ok = false;
+                J.why += "; no time left for the next stack plan";
+                sc->alts.clear();
+            } else {
+                ok = rtc_compile(src, std::max(left, 0.1 * lim.max_compile_s), J.code, J.why, J.rtc);
+                ++compiles;
+            }
         }
         if (sc->want_waves) {
-            const bool held = ok && module_holds(J.code, sc->want_waves, note);
+            const bool held = ok && module_holds(J.code, sc->want_waves, lim.vgpr_file, note);
             sc->occ_note += (sc->occ_note.empty() ? "" : ";") + (ok ? note : "w" + std::to_string(sc->want_waves) + ":declined") +
                             (held ? "" : "-rejected");
             if (!held && !sc->alts.empty()) { // the next plan
@@ -2911,8 +2929,7 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
                 sc->alts.erase(sc->alts.begin());
                 use_plan(sc, std::move(next));
                 sc->tile = sched_default_tile(sc->prog);
-                drop_sched_devices(sc);
-                J.code.clear();
+                J.code.clear(); // (tier 2 kept the default plan throughout: tier2_prog)
                 continue;
             }
         }
@@ -3001,7 +3018,13 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
         lanes = (std::max<uint64_t>(chunk, 1) + block - 1) / block * block;
         blocks = (int)(lanes / block);
     } else {
-        const uint64_t per_block = sc->jit.shape == JIT_STREAM ? block * kJitStreamLanes : block;
+        // inputs a block takes: the stream kernel's tile, the tile-sorted
+        // machine kernel's (a block holds at least one full tile), else one
+        // per thread
+        const bool sorted = sc->jit.shape == JIT_MACHINE && !sc->jit.pool && h->jit_lim.tile_sort && !h->jit_lim.order;
+        const uint64_t per_block = sc->jit.shape == JIT_STREAM ? block * kJitStreamLanes
+                                   : sorted ? block * jit_sort_rounds(h->jit_lim, P.nslots)
+                                            : block;
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
         blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
@@ -3115,7 +3138,7 @@ Tier pick_tier(mk_net *h, uint32_t cap, uint32_t flags, uint32_t budget, SchedCa
     // superblock per lane, and the interpreter is faster (census class
     // data_dependent_stack_depth, 4,098 superblocks: 0.016 T node-instr/s on
     // tier 2, 0.080 T on tier 1).  TILE / REFILL still demand tier 2.
-    if (sc->ok && sc->prog.nsb > kSchedInterpSb && !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL))) return TIER_INTERP;
+    if (sc->ok && tier2_prog(sc).nsb > kSchedInterpSb && !(flags & (MK_FLAG_TILE | MK_FLAG_REFILL))) return TIER_INTERP;
     return sc->ok ? TIER_COMPILED : TIER_INTERP;
 }
 
@@ -3286,8 +3309,10 @@ struct SessK {
     uint32_t epoch;
 };
 
+// *queued (when given) is set once a kernel has been queued on `stream`, so
+// that a caller whose launch fails part way still orders later work after it.
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
-                   hipStream_t stream, uint32_t ncalls = 1, bool resume = false)
+                   hipStream_t stream, uint32_t ncalls = 1, bool resume = false, bool *queued = nullptr)
 {
     if (s->broken) return MK_EDEVICE;
     if (s->n == 0 || ncalls == 0) return MK_OK;
@@ -3312,6 +3337,7 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
         if (hipModuleLaunchKernel(s->fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr) !=
             hipSuccess)
             return MK_EDEVICE;
+        if (queued) *queued = true;
         // 2. calls it handed off become interpreter sessions: imported by
         // the interpreter kernel itself, thread by thread, before it runs
         p.fuse_import = 1u;
@@ -3718,8 +3744,14 @@ int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t nca
     // that ran on another stream), and the session's own stream's later work
     // (reset, host calls) after this one
     if (int rc = mk::session_wait_last(s, st)) return rc;
-    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls);
-    if (rc) return rc;
+    bool queued = false;
+    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls, false, &queued);
+    if (rc) {
+        // the native kernel may be running on `st` although the launch
+        // failed after it: reset and teardown must still wait for it
+        if (queued) (void)mk::session_mark(s, st);
+        return rc;
+    }
     return mk::session_mark(s, st);
 }
 
@@ -4116,7 +4148,7 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
     if (t == mk::TIER_INTERP) {
         if (sc && sc->ok)
             snprintf(buf, sizeof buf, "tier=interp reason=compiled schedule of %u superblocks (control state follows "
-                     "the data); native tier: %s", sc->prog.nsb, sc->jit.why.c_str());
+                     "the data); native tier: %s", mk::tier2_prog(sc).nsb, sc->jit.why.c_str());
         else
             snprintf(buf, sizeof buf, "tier=interp reason=%s", sc ? sc->why.c_str() : "forced");
         return mk::copy_out(out, out_len, buf);
@@ -4128,7 +4160,8 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         (void)mk::copy_out(out, out_len, buf);
         return MK_ELIMIT;
     }
-    const mk::SchedProgram &P = sc->prog;
+    // the native tier's schedule, or tier 2's (the default plan)
+    const mk::SchedProgram &P = t == mk::TIER_NATIVE ? sc->prog : mk::tier2_prog(sc);
     int len = snprintf(buf, sizeof buf, "superblocks=%u regs=%u slots=%u words=%zu jtab=%zu rounds=%llu", P.nsb,
                        P.nregs, P.nslots, P.code.size(), P.jtab.size(), (unsigned long long)P.sym_rounds);
     std::string s;
@@ -4165,9 +4198,15 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         // resident waves per SIMD of the loaded kernel (registers and LDS;
         // the first device it is loaded on): the occupancy its issue rate is
         // priced at (bench.py roofline_issue.occupancy)
+        // (a fraction when the blocks per CU do not fill the four SIMDs
+        // evenly: 15 blocks of one wave are 3.75 per SIMD, not 3)
         for (int d = 0; d < mk::kMaxDevices; d++)
             if (sc->jit.dev[d].fn) {
-                s += " waves_per_simd=" + std::to_string(sc->jit.dev[d].per_cu * sc->jit.block / 256);
+                const int wcu = sc->jit.dev[d].per_cu * sc->jit.block / 64; // waves per CU
+                char w[32];
+                if (wcu % 4 == 0) snprintf(w, sizeof w, "%d", wcu / 4);
+                else snprintf(w, sizeof w, "%.2f", wcu / 4.0);
+                s += std::string(" waves_per_simd=") + w;
                 break;
             }
     } else {
@@ -4232,7 +4271,7 @@ int mk_net_sched_disasm(mk_net *h, const mk_opts *opts, char *out, size_t out_le
     std::lock_guard<std::mutex> lk(h->mu);
     mk::SchedCache *sc = mk::get_sched(h, cap, (flags & MK_FLAG_STOP_ON_OUTPUT) != 0);
     if (!sc->ok) return MK_ELIMIT;
-    return mk::copy_out(out, out_len, mk::sched_disasm(sc->prog));
+    return mk::copy_out(out, out_len, mk::sched_disasm(mk::tier2_prog(sc)));
 }
 
 int mk_net_info(const mk_net *net, int *counts3)

@@ -1650,16 +1650,41 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             e.line("    L.steps += %uu;", I.inc);
             e.line("    {");
             w.jro_target(I);
-            const uint32_t last = p.jtab[(size_t)I.imm + I.b];
-            std::string sel;
-            for (uint32_t t = 0; t < I.b; ++t) {
-                const uint32_t tgt = p.jtab[(size_t)I.imm + t];
-                if (tgt == last) continue;
-                char b[64];
-                snprintf(b, sizeof b, "t == %u ? %uu : ", t, tgt);
-                sel += b;
+            // The successor table packed into at most four 64-bit constants
+            // (W-bit entries, 64 / W per word): a select of the word and a
+            // shift (round 6).  The select chain below it LLVM turns into a
+            // switch, which a divergent t lowers as a tree of exec-masked
+            // branches: ~120 instructions for C5's 15 arms.
+            uint32_t top = 0;
+            for (uint32_t t = 0; t <= I.b; ++t) top = std::max(top, p.jtab[(size_t)I.imm + t]);
+            const uint32_t W = top < 16u ? 4u : top < 256u ? 8u : 16u, P = 64u / W;
+            const uint32_t words = (I.b + 1u + P - 1u) / P;
+            if (top < 65536u && words <= 4u) {
+                std::string sel;
+                for (uint32_t k = 0; k < words; ++k) {
+                    uint64_t word = 0;
+                    for (uint32_t t = k * P; t < (k + 1u) * P && t <= I.b; ++t)
+                        word |= (uint64_t)p.jtab[(size_t)I.imm + t] << (W * (t - k * P));
+                    char b[96];
+                    if (k + 1u < words) snprintf(b, sizeof b, "ti < %uu ? 0x%016llxull : ", (k + 1u) * P, (unsigned long long)word);
+                    else snprintf(b, sizeof b, "0x%016llxull", (unsigned long long)word);
+                    sel += b;
+                }
+                e.line("        const uint32_t ti = (uint32_t)t;");
+                e.line("        const uint64_t tw = %s;", sel.c_str());
+                e.line("        L.sb = (uint32_t)(tw >> (%uu * (ti & %uu))) & 0x%xu;", W, P - 1u, (1u << W) - 1u);
+            } else {
+                const uint32_t last = p.jtab[(size_t)I.imm + I.b];
+                std::string sel;
+                for (uint32_t t = 0; t < I.b; ++t) {
+                    const uint32_t tgt = p.jtab[(size_t)I.imm + t];
+                    if (tgt == last) continue;
+                    char b[64];
+                    snprintf(b, sizeof b, "t == %u ? %uu : ", t, tgt);
+                    sel += b;
+                }
+                e.line("        L.sb = %s%uu;", sel.c_str(), last);
             }
-            e.line("        L.sb = %s%uu;", sel.c_str(), last);
             e.line("    }");
             break;
         }
@@ -2084,45 +2109,40 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 )";
 
 // Kernel of the machine shape with lanes grouped by value inside a tile.
-// A block takes tiles of MK_TS_T = 1024 contiguous inputs (grid-stride):
-//   1. loads them (coalesced) and buckets them by value in LDS: block
-//      min / max, 256 buckets of equal width (a power of two), an LDS
-//      histogram, its prefix sum and a scatter -- a counting sort whose
-//      order inside a bucket does not matter;
-//   2. runs them in sorted order, 64 at a time per wave (four rounds, the
-//      waves' chunks in snake order so that each wave's four chunks
-//      balance), every chunk by generations (mk_run on the superblock of the
-//      lowest running lane until every lane of the chunk has ended);
-//   3. writes the tile's out / status / steps back through LDS, coalesced.
+// A block takes tiles of MK_TS_T = 256 R contiguous inputs (grid-stride):
+//   1. loads them (coalesced: thread t holds inputs t, t + 256, ...) and
+//      buckets them by value in LDS: block min / max, 256 buckets of equal
+//      width (a power of two), an LDS histogram, its prefix sum and a
+//      scatter of (position, input) pairs, one 64-bit word each -- a
+//      counting sort whose order inside a bucket does not matter;
+//   2. runs them in sorted order, 64 at a time per wave (R rounds, the
+//      waves' chunks in snake order so that each wave's chunks balance),
+//      every chunk by sweeps then generations (mk_run on the superblock of
+//      the lowest running lane until every lane of the chunk has ended); each
+//      lane stores its out / status / steps straight to its input's position
+//      (the tile's 4 KiB of outputs are whole lines in L2 before they leave).
 // Equal inputs take identical paths, and where trip counts follow the input
 // (C5's countdowns, the census classes' push loops) a chunk's lanes leave
 // their loops together: the idle lanes of generations over unsorted inputs
 // (a wave runs each loop for its longest trip) mostly go away, without the
 // global sort's atomics and scattered result writes (MK_JIT_ORDER).
+// LDS bank conflicts come only from operations at data-dependent addresses
+// (the histogram and rank atomics, the scatter); round 6 halved them per
+// input (7 -> 3: no results through LDS, one 64-bit scatter in place of a
+// 32- and a 16-bit one) and made the scatter of equal or presorted inputs
+// conflict-free (the strided layout; R consecutive inputs per thread made it
+// 4-way).
 static const char *const kMachineSortKernel = R"(
 #define MK_TS_T (256u * MK_TS_R)
 #define MK_TS_NB 256u
-// MK_JIT_TS_WAVES asks the allocator for that many waves per SIMD on small
-// lane states (C5 at 8: 79 -> 63 VGPRs, yet 220 vs 215 us: off by default).
-#if MK_LANE_REGS <= 8 && MK_TS_WAVES_N
-#define MK_TS_WAVES __attribute__((amdgpu_waves_per_eu(MK_TS_WAVES_N)))
-#else
-#define MK_TS_WAVES
-#endif
-extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParams p)
+extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 {
-    __shared__ int32_t s_key[MK_TS_T];
-    __shared__ int32_t s_out[MK_TS_T];
-    __shared__ uint32_t s_steps[MK_TS_T];
-    __shared__ uint16_t s_pos[MK_TS_T];
-    __shared__ uint8_t s_st[MK_TS_T];
+    __shared__ uint64_t s_kp[MK_TS_T]; // the tile in sorted order: position << 32 | input
     __shared__ uint32_t s_cnt[MK_TS_NB];
     __shared__ uint32_t s_red[8];
-    __shared__ uint32_t s_next; // MK_TS_DYN: the tile's next chunk
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
     const uint32_t pol = MK_POLICY;
-    (void)wave;
     // counters: steps per lane (one wave sum at the end), the others
     // wave-uniform (scalar registers): outputs, lanes, and the four end reasons
     uint64_t c_steps = 0u;
@@ -2132,36 +2152,30 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
     // MK_JIT_PROF: shader-clock cycles per phase, per wave, in place of the
     // counters (tools/probe/c5_decomp.py reads them from the stats)
     const uint64_t pf_t0 = MK_T();
-    uint64_t pf_sort = 0u, pf_chunk = 0u, pf_loop = 0u, pf_other = 0u, pf_res = 0u, pf_rounds = 0u, pf_lrounds = 0u;
+    uint64_t pf_sort = 0u, pf_chunk = 0u, pf_loop = 0u, pf_other = 0u, pf_rounds = 0u, pf_lrounds = 0u;
 #endif
     const uint64_t ntiles = (p.n + MK_TS_T - 1) / MK_TS_T;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * MK_TS_T;
         const uint32_t m = p.n - base < MK_TS_T ? (uint32_t)(p.n - base) : MK_TS_T;
-        const bool vec = p.io_vec && m == MK_TS_T;
 #if MK_PROF
         uint64_t pf_a = MK_T();
 #endif
-        // 1. inputs R tid .. R tid + R - 1 of the tile, their range
+        // 1. inputs tid + 256 k of the tile, their range
         int32_t v[MK_TS_R];
-        if (vec) {
-            for (uint32_t k = 0; k < MK_TS_R; k += 4u) {
-                const int4 q = *reinterpret_cast<const int4 *>((const int32_t *)p.in_data + base + MK_TS_R * tid + k);
-                v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
-            }
+        if (p.io_vec && m == MK_TS_T) {
+            for (uint32_t k = 0; k < MK_TS_R; ++k) v[k] = ((const int32_t *)p.in_data)[base + tid + 256u * k];
         } else {
-            for (uint32_t k = 0; k < MK_TS_R; ++k)
-                v[k] = MK_TS_R * tid + k < m ? sched_input(p, base + MK_TS_R * tid + k) : 0;
+            for (uint32_t k = 0; k < MK_TS_R; ++k) v[k] = tid + 256u * k < m ? sched_input(p, base + tid + 256u * k) : 0;
         }
         uint32_t lo = 0xFFFFFFFFu, hi = 0u; // biased: signed order as unsigned
         for (uint32_t k = 0; k < MK_TS_R; ++k) {
-            if (MK_TS_R * tid + k >= m) continue;
+            if (tid + 256u * k >= m) continue;
             const uint32_t b = (uint32_t)v[k] ^ 0x80000000u;
             lo = b < lo ? b : lo;
             hi = b > hi ? b : hi;
         }
         s_cnt[tid] = 0u;
-        if (tid == 0u) s_next = 0u;
         lo = MK_WAVE_MIN(lo);
         hi = MK_WAVE_MAX(hi);
         if (lane == 0u) {
@@ -2180,10 +2194,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         uint32_t bk[MK_TS_R];
         for (uint32_t k = 0; k < MK_TS_R; ++k) {
             // a tile of one value (span 0) goes by position, bucket tid: its
-            // 1,024 atomics on one bucket would serialize (C5 with every input
-            // 0 spent half its time here, profiles/r04r_c5_phase_prof.jsonl)
+            // inputs' atomics on one bucket would serialize (C5 with every
+            // input 0 spent half its time here, profiles/r04r_c5_phase_prof.jsonl)
             bk[k] = span ? (((uint32_t)v[k] ^ 0x80000000u) - lo) >> sh : tid;
-            if (MK_TS_R * tid + k < m) atomicAdd(&s_cnt[bk[k]], 1u);
+            if (tid + 256u * k < m) atomicAdd(&s_cnt[bk[k]], 1u);
         }
         __syncthreads();
         // exclusive prefix sum over the 256 buckets (thread tid owns bucket tid)
@@ -2202,36 +2216,24 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
             __syncthreads();
         }
         for (uint32_t k = 0; k < MK_TS_R; ++k) {
-            if (MK_TS_R * tid + k >= m) continue;
+            if (tid + 256u * k >= m) continue;
             const uint32_t d = atomicAdd(&s_cnt[bk[k]], 1u);
-            s_key[d] = v[k];
-            s_pos[d] = (uint16_t)(MK_TS_R * tid + k);
+            s_kp[d] = (uint64_t)(tid + 256u * k) << 32 | (uint32_t)v[k];
         }
         __syncthreads();
 #if MK_PROF
         pf_sort += MK_T() - pf_a;
         pf_a = MK_T();
 #endif
-        // 2. the sorted lanes, 64 per chunk: MK_TS_DYN -- a wave that is
-        // free takes the next chunk, highest values first (their loops run
-        // longest where trips follow the value), so the waves reach the
-        // tile's closing barrier together; else each wave's chunks in snake
-        // order
-        for (uint32_t r = 0;; ++r) {
-#if MK_TS_DYN
-            uint32_t cn = 0u;
-            if (lane == 0u) cn = atomicAdd(&s_next, 1u);
-            cn = (uint32_t)__builtin_amdgcn_readfirstlane((int)cn);
-            if (cn >= 4u * MK_TS_R) break;
-            const uint32_t c = 4u * MK_TS_R - 1u - cn;
-#else
-            if (r >= MK_TS_R) break;
+        // 2. the sorted lanes, 64 per chunk, each wave's chunks in snake order
+        // (the next tile's first barrier keeps s_kp until every wave is done)
+        for (uint32_t r = 0; r < MK_TS_R; ++r) {
             const uint32_t c = r * 4u + ((r & 1u) ? 3u - wave : wave);
-#endif
             const uint32_t j = c * 64u + lane;
             const bool live = j < m;
+            const uint64_t kp = live ? s_kp[j] : 0u;
             MkLane L;
-            mk_init(L, live ? s_key[j] : 0);
+            mk_init(L, (int32_t)(uint32_t)kp);
             if (!live) L.sb = MK_SB_IDLE;
 #if defined(MK_SWEEP_LIST)
             // sweep dispatch (MK_JIT_SWEEP): the variants in forward order,
@@ -2272,10 +2274,10 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 #endif
             }
             if (live) {
-                const uint32_t at = s_pos[j];
-                s_out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
-                s_st[at] = (uint8_t)L.st;
-                s_steps[at] = L.steps;
+                const uint64_t at = base + (kp >> 32);
+                p.out[at] = (L.st & MK_ST_HAS_OUTPUT) ? L.outv : 0;
+                p.status[at] = (uint8_t)L.st;
+                if (p.steps) p.steps[at] = L.steps;
             }
             const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
             c_steps += live ? (uint64_t)L.steps : 0u;
@@ -2288,27 +2290,6 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         }
 #if MK_PROF
         pf_chunk += MK_T() - pf_a;
-        pf_a = MK_T();
-#endif
-        __syncthreads();
-        // 3. results of the tile, in input order
-        if (vec) {
-            for (uint32_t i = 4u * tid; i < MK_TS_T; i += 1024u) {
-                MK_IO_ST(reinterpret_cast<mk_i32x4 *>(p.out + base + i), (mk_i32x4{s_out[i], s_out[i + 1], s_out[i + 2], s_out[i + 3]}));
-                MK_IO_ST(reinterpret_cast<uint32_t *>(p.status + base + i),
-                         (uint32_t)s_st[i] | (uint32_t)s_st[i + 1] << 8 | (uint32_t)s_st[i + 2] << 16 | (uint32_t)s_st[i + 3] << 24);
-                if (p.steps) *reinterpret_cast<uint4 *>(p.steps + base + i) = make_uint4(s_steps[i], s_steps[i + 1], s_steps[i + 2], s_steps[i + 3]);
-            }
-        } else {
-            for (uint32_t i = tid; i < m; i += 256u) {
-                p.out[base + i] = s_out[i];
-                p.status[base + i] = s_st[i];
-                if (p.steps) p.steps[base + i] = s_steps[i];
-            }
-        }
-        __syncthreads(); // the next tile reuses the LDS arrays
-#if MK_PROF
-        pf_res += MK_T() - pf_a;
 #endif
     }
 #if MK_PROF
@@ -2319,7 +2300,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
         q[2] += pf_chunk;
         q[3] += pf_loop;
         q[4] += pf_other;
-        q[5] += pf_res;
+        q[5] += 0u; // (no results phase since round 6)
         q[6] += pf_rounds;
         q[7] += pf_lrounds;
     }
@@ -2339,6 +2320,7 @@ extern "C" __global__ void __launch_bounds__(256) MK_TS_WAVES mk_jit_exec(SParam
 #endif
 }
 )";
+
 
 JitLimits JitLimits::from_env()
 {
@@ -2376,7 +2358,6 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_POOL", l.pool);
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
-    num("MK_JIT_TS_WAVES", l.ts_waves);
     num("MK_JIT_TS_ROUNDS", l.ts_rounds);
     if (const char *v = std::getenv("MK_JIT_LDS_SLOTS"); v && *v) {
         l.lds_slot_bytes = (size_t)std::strtoull(v, nullptr, 10);
@@ -2384,7 +2365,8 @@ JitLimits JitLimits::from_env()
     }
     num("MK_JIT_SAT_BLOCK", l.sat_block);
     if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
-    flag("MK_JIT_TS_DYN", l.ts_dyn);
+    num("MK_JIT_VGPR_FILE", l.vgpr_file);
+    if (!l.vgpr_file || l.vgpr_file > 512) l.vgpr_file = 512;
     flag("MK_JIT_SWEEP", l.sweep);
     flag("MK_JIT_SWEEP_COLD", l.sweep_cold);
     num("MK_JIT_SWEEP_PASSES", l.sweep_passes);
@@ -2407,10 +2389,10 @@ std::string JitLimits::key() const
     char b[256];
     snprintf(b, sizeof b,
              "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsw=%u,tsr=%u,lds=%zu%s,tsd=%d,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d,sblk=%u",
+             "tsort=%d,tsr=%u,lds=%zu%s,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d,sblk=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
              loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
-             (int)tile_sort, ts_waves, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "", (int)ts_dyn,
+             (int)tile_sort, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "",
              (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
     std::string k = b;
     if (!sat_count) k += ",scount=0";
@@ -2421,6 +2403,7 @@ std::string JitLimits::key() const
     if (prof) k += ",prof=1";
     if (!prio) k += ",prio=0";
     if (!sat_tier) k += ",stier=0";
+    if (vgpr_file != 512) k += ",vfile=" + std::to_string(vgpr_file);
     return k;
 }
 
@@ -2745,10 +2728,8 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     // machine-shape policy word, a constant of the module so that the loop
     // exit tests fold (generational: MK_KEEP is "some lane still looping")
     e.line("#define MK_POLICY 0x%08xu", lim.policy);
-    e.line("#define MK_TS_WAVES_N %u", lim.ts_waves); // kMachineSortKernel occupancy target (0: none)
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
-    e.line("#define MK_TS_DYN %d", lim.ts_dyn ? 1 : 0); // kMachineSortKernel: chunks taken by free waves
     if (shape == JIT_MACHINE) // machine kernels: sweep passes before rounds (stream modules' sources as they were)
         e.line("#define MK_SWEEP_PASSES %uu", lim.sweep_passes);
     if (lim.prof) { // kMachineSortKernel: cycles per phase in place of the counters (MK_JIT_PROF)

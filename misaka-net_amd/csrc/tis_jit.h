@@ -98,10 +98,6 @@ struct JitLimits {
     // 1024 (an LDS counting sort, kMachineSortKernel) so that a wave's lanes
     // have similar loop trip counts (MK_JIT_TILE_SORT=0: input order).
     bool tile_sort = true;
-    // Its occupancy target for small lane states (waves per SIMD handed to
-    // the register allocator, MK_JIT_TS_WAVES; 0: the compiler's choice --
-    // measured best: C5 215 us vs 220 at 8 and 243 at 6, r02l).
-    uint32_t ts_waves = 0;
     // Its tile: 256 x ts_rounds inputs, each wave running ts_rounds sorted
     // chunks of 64 per tile (MK_JIT_TS_ROUNDS = 4, 8 or 16).  r02v: 8 is 2%
     // faster on C5 (211 vs 215 us) but 20% / 8% slower on the dynamic-stack
@@ -113,10 +109,6 @@ struct JitLimits {
     // Stream shape: registers whose high 32 bits nothing reads are computed
     // in 32 bits (narrow_regs in tis_jit.cpp; MK_JIT_NARROW=0: all int64).
     bool narrow = true;
-    // Its chunks: taken by whichever wave of the block is free, highest
-    // values first (MK_JIT_TS_DYN=1), instead of four per wave in snake
-    // order.
-    bool ts_dyn = false;
     // kMachineSortKernel dispatches by sweeps over the variants in reverse
     // postorder (tis_jit.cpp forward_order), each variant one ballot when no
     // lane is on it, instead of one variant per round (MK_JIT_SWEEP=0: rounds;
@@ -186,6 +178,12 @@ struct JitLimits {
     // C5 111.1 / 111.6 -> 105.3 / 105.3 us (r05s); GPU parity subset green with it.
     bool sat_tier = true;
 
+    // VGPRs per SIMD lane a module's waves share when a stack plan's module
+    // is checked against its waves per SIMD (mk_exec.hip module_holds):
+    // gfx950's 512.  MK_JIT_VGPR_FILE lowers it so that tests reach the
+    // rejection path (the next plan, last the default) on purpose.
+    uint32_t vgpr_file = 512;
+
     static JitLimits from_env();
     // The knobs that change generated code, as text (the module cache key
     // and the `knobs=` field of mk_net_plan).
@@ -227,6 +225,13 @@ uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim);
 // lim.policy (the machine shape's policy word) is compiled in.
 std::string jit_module_source(const std::string &lane_src, JitShape shape, bool heavy, const JitLimits &lim,
                               uint32_t pool = 0);
+
+// Lanes per thread per tile of the tile-sorted machine kernel (MK_TS_R):
+// JitLimits::ts_rounds, or by the lane's stack slots when that is 0.
+inline uint32_t jit_sort_rounds(const JitLimits &lim, uint32_t nslots)
+{
+    return lim.ts_rounds ? lim.ts_rounds : nslots ? 4u : 8u;
+}
 
 // Name of the generated kernel.
 constexpr const char *kJitKernel = "mk_jit_exec";

@@ -43,30 +43,72 @@ def gather_outputs(out, dist, dst: int = 0):
     return None
 
 
-def timed_gather(step, out, status, dist, steps: int, sync=None):
+def pack_views(buf, lanes: int):
+    """The int32 outputs and u8 statuses of one rank's step as views of one
+    packed buffer (uint8[5 * lanes]: 4 * lanes bytes of outputs, then the
+    status bytes), so that a step's results leave the rank in ONE collective.
+    The status view starts 4 * lanes bytes in: 4-byte aligned, as the
+    executor's vector stores need."""
+    import torch
+
+    assert buf.dtype == torch.uint8 and buf.numel() == 5 * lanes
+    return buf[: 4 * lanes].view(torch.int32), buf[4 * lanes:]
+
+
+def unpack_gathered(g, lanes: int, world: int):
+    """Rank 0: the (outputs int32[world * lanes], statuses u8[world * lanes])
+    in global lane order from the gathered packed rows (pack_views' layout)."""
+    import torch
+
+    rows = g.view(world, 5 * lanes)
+    out = rows[:, : 4 * lanes].contiguous().view(torch.int32).reshape(-1)
+    return out, rows[:, 4 * lanes:].reshape(-1)
+
+
+def timed_gather(step, bufs, dist, steps: int, sync=None):
     """End-to-end leg of an N-rank run (SURVEY.md section 8 row e): `steps`
-    times, run one step (`step()`, the launch that fills this rank's `out`
-    int32 and `status` u8 shards) and gather both to rank 0 in global lane
-    order.  Returns (seconds, the max over ranks; gathered out; gathered
-    status), the gathered tensors on rank 0 and None elsewhere.  `sync`
-    waits for the device (torch.cuda.synchronize); None on CPU."""
+    times, run one step (`step(b)`: the launch that fills this rank's packed
+    results buffer `bufs[b]`, pack_views' layout) and gather that buffer to
+    rank 0 in global lane order: one collective per step.  The buffers
+    alternate (b = k % 2) and each gather is issued asynchronously, so the
+    gather of step k runs while step k + 1 computes (RCCL's stream waits for
+    the step's launch; the launch that rewrites a buffer waits for its
+    previous gather).  Returns (seconds, the max over ranks; the gathered
+    packed rows of the last step), the rows on rank 0 and None elsewhere.
+    `sync` waits for the device (torch.cuda.synchronize); None on CPU."""
     import time
 
     import torch
 
     sync = sync or (lambda: None)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    gloo = dist.get_backend() == "gloo"  # gloo gathers host tensors only
+    n = bufs[0].numel()
+    rdev = torch.device("cpu") if gloo else bufs[0].device
+    recv = [torch.empty(world * n, dtype=torch.uint8, device=rdev) for _ in bufs] if rank == 0 else None
+    pending, keep = [None] * len(bufs), [None] * len(bufs)
     sync()
     dist.barrier()
     t0 = time.perf_counter()
-    g_out = g_st = None
-    for _ in range(steps):
-        step()
-        g_out = gather_outputs(out, dist)
-        g_st = gather_outputs(status, dist)
+    for k in range(steps):
+        b = k % len(bufs)
+        if pending[b] is not None:
+            pending[b].wait()  # the gather still reading bufs[b]
+        step(b)
+        src = bufs[b].cpu() if gloo and bufs[b].is_cuda else bufs[b]
+        keep[b] = src  # alive until its gather completes
+        gl = list(recv[b].view(world, n).unbind(0)) if rank == 0 else None
+        pending[b] = dist.gather(src, gather_list=gl, dst=0, async_op=True)
+    for w in pending:
+        if w is not None:
+            w.wait()
     sync()
-    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=out.device)
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=bufs[0].device if not gloo else "cpu")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    return tt.item(), g_out, g_st
+    last = None
+    if rank == 0 and steps:
+        last = recv[(steps - 1) % len(bufs)].to(bufs[0].device)
+    return tt.item(), last
 
 
 def verify_gathered(g_out, g_st, full) -> bool:

@@ -38,22 +38,27 @@ def _worker(rank, world, port, q):
     out, st, sp = po.OracleNet(mk.networks.sample_network()).compute_batch(xs)
     stats = torch.tensor([int(sp.sum()), int(((st & 0x10) != 0).sum()), hi - lo, 0, 0, 0, 0, 0], dtype=torch.int64)
     mk.dist.reduce_counters(stats, dist)
-    g = mk.dist.gather_outputs(torch.from_numpy(out), dist)
+    gathered = mk.dist.gather_outputs(torch.from_numpy(out), dist)
     # bench.py's end-to-end leg, the code an N-GPU run executes: K steps of
-    # (fill this rank's shard, ordered gather of out + status to rank 0),
-    # timed as the max over ranks, then rank 0 checks the gathered batch
-    # against one evaluation over all global lanes
-    o_t, s_t = torch.zeros(hi - lo, dtype=torch.int32), torch.zeros(hi - lo, dtype=torch.uint8)
+    # (fill this rank's packed out + status buffer, one ordered gather of it
+    # to rank 0, overlapped with the next step), timed as the max over ranks,
+    # then rank 0 checks the gathered batch against one evaluation over all
+    # global lanes
+    n = hi - lo
+    bufs = [torch.zeros(5 * n, dtype=torch.uint8) for _ in range(2)]
     calls = []
 
-    def step():
-        calls.append(1)
-        o_t.copy_(torch.from_numpy(out))
-        s_t.copy_(torch.from_numpy(st))
+    def step(b):
+        calls.append(b)
+        o_v, s_v = mk.dist.pack_views(bufs[b], n)
+        o_v.copy_(torch.from_numpy(out))
+        s_v.copy_(torch.from_numpy(st))
 
-    secs, g_out, g_st = mk.dist.timed_gather(step, o_t, s_t, dist, 3)
-    verified = None
+    secs, g = mk.dist.timed_gather(step, bufs, dist, 3)
+    verified = caught = None
     if rank == 0:
+        g_out, g_st = mk.dist.unpack_gathered(g, n, world)
+
         def full():
             xa = po.gen_inputs(SEED, world * LANES)
             fo, fs, _ = po.OracleNet(mk.networks.sample_network()).compute_batch(xa)
@@ -63,10 +68,13 @@ def _worker(rank, world, port, q):
         wrong = g_out.clone()
         wrong[LANES] ^= 1  # a lane of rank 1's shard: a gather out of order or short would differ too
         caught = not mk.dist.verify_gathered(wrong, g_st, full)
+        wrong_st = g_st.clone()
+        wrong_st[2 * LANES - 1] ^= 0x10  # the last status byte of rank 1's packed row
+        caught = caught and not mk.dist.verify_gathered(g_out, wrong_st, full)
     else:
-        assert g_out is None and g_st is None
+        assert g is None
     if rank == 0:
-        q.put((stats.numpy().tolist(), g.numpy().tolist(), secs > 0 and len(calls) == 3, verified, caught))
+        q.put((stats.numpy().tolist(), gathered.numpy().tolist(), secs > 0 and calls == [0, 1, 0], verified, caught))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -197,6 +205,12 @@ def test_bench_reads_only_shipped_profiles():
         assert os.path.exists(os.path.join(root, rel))
         for p in pats:
             assert not fnmatch.fnmatch("./" + rel, p) and not fnmatch.fnmatch(rel, p.lstrip("./")), (rel, p)
-    occ = bench.occupancy_cap(6)
-    assert occ["measured_at_waves_per_simd"] == 4 and occ["cap"] > 40
-    assert bench.occupancy_cap(1)["cap"] < 30 and bench.occupancy_cap(0) is None
+    # round 6: a measured row at every occupancy 1..8,
+    # so a line is priced at its own; a fraction at its whole part
+    for w in range(1, 9):
+        occ = bench.occupancy_cap(w)
+        assert occ["measured_at_waves_per_simd"] == w == occ["waves_per_simd"], occ
+    assert bench.occupancy_cap(6)["cap"] > 40 and bench.occupancy_cap(1)["cap"] < 30
+    occ = bench.occupancy_cap(3.75)
+    assert occ["measured_at_waves_per_simd"] == 3 and occ["waves_per_simd"] == 3.75
+    assert bench.occupancy_cap(0) is None

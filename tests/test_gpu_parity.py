@@ -514,6 +514,39 @@ def test_c4_observe_full_size_every_lane(gpu, depth, n):
     assert (st == 0x11).all() and (sp == ref[2][0]).all() and stats[0] == int(ref[2][0]) * n
 
 
+# The stack plans the loader falls back to: with the register
+# file the check prices against lowered (MK_JIT_VGPR_FILE), D=256 runs its
+# two-wave plan (256) or the default one-wave plan (128) -- every lane at the
+# bench size, as test_c4_observe_full_size_every_lane -- and tier 2 runs the
+# default plan's schedule while the native tier runs a more_waves plan.
+@pytest.mark.parametrize("vfile,plans", [(256, "w2:"), (128, "-rejected;w2:")])
+def test_c4_stack_plan_fallbacks_every_lane(gpu, monkeypatch, vfile, plans):
+    monkeypatch.setenv("MK_JIT_VGPR_FILE", str(vfile))
+    nodes = mk.networks.pipeline_network(256, observe=True)
+    net = mk.Network(nodes)
+    plan = net.plan()
+    assert plans in plan and ("regs=64" in plan) == (vfile == 128), plan
+    n = 1 << 19
+    out, st, sp, stats = _device_run(net, n)
+    x = po.gen_inputs(SEED, n)
+    A, B = _affine(nodes)
+    _assert_affine_every_lane(out, x, A, B)
+    ref = oracle(nodes, x[:512])
+    assert np.array_equal(out[:512], ref[0]) and np.array_equal(sp[:512], ref[2])
+    assert (st == 0x11).all() and stats[0] == int(ref[2][0]) * n
+
+
+def test_tier2_keeps_the_default_stack_plan(gpu):
+    nodes = mk.networks.pipeline_network(256, observe=True)
+    net = mk.Network(nodes)
+    regs = lambda plan: int(plan.split("regs=")[1].split()[0])  # noqa: E731
+    assert regs(net.plan()) > 200 and regs(net.plan(mode="tile")) == 64, (net.plan(), net.plan(mode="tile"))
+    xs = po.gen_inputs(SEED, 20000)
+    ref = oracle(nodes, xs)
+    for mode in ("tile", "refill", None):
+        assert_same(net.compute_batch(xs, mode=mode), ref, f"C4 d256 {mode}")
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_wide_immediates_on_symbolic_acc(gpu, mode):
     # immediates whose low 32-bit word has bit 31 set, applied to a data-dependent ACC

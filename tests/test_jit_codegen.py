@@ -234,14 +234,18 @@ def test_machine_shape_pipeline_compiles_in_bound(depth, monkeypatch):
 def test_pipeline_stacks_share_slots(monkeypatch):
     # node k drains its stack before node k+1 pushes: the eight stacks share
     # one slot range (tis_sched.cpp share_slots); MK_SCHED_SHARE=0 gives each
-    # its own.  D=64's shared range fits LDS: the heavy kernel keeps it there.
+    # its own.  D=64's shared range fits LDS: the heavy kernel keeps it there
+    # (its default plan: round 6 also plans eight waves per SIMD, with 16
+    # slots -- test_lds_occupancy_tunes_register_count).
     for depth, shared, own in ((64, 41, 328), (256, 233, 1864), (1024, 1001, 8008)):
         assert sc.jit_lane(mk.networks.pipeline_network(depth))[1] == shared
         monkeypatch.setenv("MK_SCHED_SHARE", "0")
         assert sc.jit_lane(mk.networks.pipeline_network(depth))[1] == own
         monkeypatch.delenv("MK_SCHED_SHARE")
+    monkeypatch.setenv("MK_JIT_VGPR_FILE", "256")  # the eight-wave plan rejected: the default
     plan = mk.Network(mk.networks.pipeline_network(64)).plan(mode="jit")
     assert "slots=41 " in plan and "shape=stream-heavy-lds " in plan, plan
+    monkeypatch.delenv("MK_JIT_VGPR_FILE")
     monkeypatch.setenv("MK_JIT_LDS_SLOTS", "0")
     plan = mk.Network(mk.networks.pipeline_network(64)).plan(mode="jit")
     assert "shape=stream-heavy " in plan, plan
@@ -249,7 +253,8 @@ def test_pipeline_stacks_share_slots(monkeypatch):
 
 def test_lds_occupancy_tunes_register_count(monkeypatch):
     # The loader's policy for heavy networks (mk_exec.hip tune_lds_auto):
-    # D=64's 41 slots fit LDS at four waves per CU: kept, 24 registers; D=256
+    # D=64's 41 slots fit LDS at four waves per CU, yet eight per SIMD take
+    # 49 registers (16 slots in a 5 KiB share, round 6); D=256
     # gets eight waves per SIMD (more_waves): 241 registers leave 16 slots,
     # all in a 5 KiB LDS share, and the compiled module holds eight waves
     # (its VGPRs are checked: stack_plans=w8:...); D=300 cannot reach eight
@@ -260,8 +265,9 @@ def test_lds_occupancy_tunes_register_count(monkeypatch):
         plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode="jit")
         return dict(w.split("=", 1) for w in plan.split() if "=" in w)
 
-    f = fields(64)
-    assert f["shape"] == "stream-heavy-lds" and f["regs"] == "24" and f["slots"] == "41", f
+    f = fields(64)  # round 6: eight waves per SIMD too (49 registers, 16 slots in a 5 KiB share)
+    assert f["shape"] == "stream-heavy-lds" and f["regs"] == "49" and f["slots"] == "16", f
+    assert f["stack_plans"].startswith("w8:") and "rejected" not in f["stack_plans"], f
     f = fields(256)
     assert f["shape"] == "stream-heavy-lds" and f["regs"] == "241" and f["slots"] == "16", f
     assert f["stack_plans"].startswith("w8:") and "rejected" not in f["stack_plans"], f
@@ -283,6 +289,37 @@ def test_lds_occupancy_tunes_register_count(monkeypatch):
     assert f["slots"] == "233" and f["regs"] == "24", f
 
 
+def test_stack_plan_rejection_falls_back(monkeypatch):
+    # The plan-rejection path of jit_compile: a more_waves plan
+    # whose module cannot hold its waves gives way to the next plan, and last
+    # to the default.  MK_JIT_VGPR_FILE lowers the register file the check
+    # prices against, so the path runs on purpose: at 256 VGPRs D=256's
+    # eight-wave module (38 VGPRs x 8 = 304) is rejected and the two-wave
+    # plan (80 slots in LDS) compiles and holds; at 128 both are rejected and
+    # the default (64 registers, 160 of 193 slots in LDS) runs.
+    def fields(depth, mode="jit"):
+        plan = mk.Network(mk.networks.pipeline_network(depth)).plan(mode=mode)
+        return dict(w.split("=", 1) for w in plan.split() if "=" in w)
+
+    monkeypatch.setenv("MK_JIT_VGPR_FILE", "256")
+    f = fields(256)
+    assert f["stack_plans"].startswith("w8:") and f["stack_plans"].split(";")[0].endswith("-rejected"), f
+    assert f["stack_plans"].split(";")[1].startswith("w2:") and "rejected" not in f["stack_plans"].split(";")[1], f
+    assert int(f["slots"]) <= 80 and f["shape"] == "stream-heavy-lds", f
+    monkeypatch.setenv("MK_JIT_VGPR_FILE", "128")
+    f = fields(256)
+    assert f["stack_plans"].count("-rejected") == 2, f
+    assert f["regs"] == "64" and f["slots"] == "193" and f["shape"] == "stream-heavy-split", f
+    f = fields(64)  # D=64's eight-wave plan rejected: the 24-register default (41 slots, 15 waves per CU)
+    assert f["stack_plans"].endswith("-rejected") and f["regs"] == "24" and f["slots"] == "41", f
+    # tier 2 keeps the default plan whichever plan the native tier runs: its
+    # LDS register file would hold one block per CU at 241 registers
+    monkeypatch.delenv("MK_JIT_VGPR_FILE")
+    assert fields(256)["regs"] == "241"
+    t2 = fields(256, mode="tile")
+    assert t2["regs"] == "64" and t2["slots"] == "193" and t2["B"] == "64", t2
+
+
 def test_compile_bounds_fall_back_with_reason(monkeypatch):
     # over the source bound: tier 2 runs it, mk_net_plan names the bound
     monkeypatch.setenv("MK_JIT_MAX_SRC", "1000")
@@ -293,8 +330,11 @@ def test_compile_bounds_fall_back_with_reason(monkeypatch):
     # over the time bound: the compile is abandoned, tier 2 runs it
     monkeypatch.delenv("MK_JIT_MAX_SRC")
     monkeypatch.setenv("MK_JIT_COMPILE_S", "0.001")
+    # (one bound for all its stack plans' compiles together: the first one
+    # abandoned, none is started for the next)
     plan = mk.Network(mk.networks.pipeline_network(256)).plan()
     assert plan.startswith("tier=compiled ") and "did not finish" in plan, plan
+    assert "no time left for the next stack plan" in plan and "regs=64" in plan, plan
 
 
 @pytest.mark.parametrize("cls", ["data_dependent_stack_depth", "two_stacks_independent_depths"])

@@ -234,7 +234,7 @@ int main()
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (const K &k : kernels) {
-        for (int w : {1, 2, 4, 8}) {
+        for (int w = 1; w <= 8; ++w) {
             const int blocks = 256 * w;
             hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(256), 0, 0, in, out, iters); // warm
             (void)hipEventRecord(e0, 0);
