@@ -23,6 +23,7 @@
 // Semantics restated from internal/nodes/program.go:219-566,
 // internal/nodes/stack.go:95-155, internal/nodes/master.go:233-249 and
 // internal/utils/math.go:20-22; see tis_front.cpp for the lowering.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -1807,7 +1808,7 @@ uint32_t lds_waves(const SchedProgram &P, const JitLimits &lim)
     if (!jit_slots_in_lds(P.nslots, true, lim)) return 0;
     // LDS allocation granule: measured, 207 slots (52,992 B) fit three waves per
     // CU and 212 (54,272 B) do not (r02af), so a 2 KiB granule is assumed
-    const uint64_t bytes = ((uint64_t)jit_lds_words(P.nslots, lim.lds_quad) * 256u + 2047u) / 2048u * 2048u;
+    const uint64_t bytes = ((uint64_t)P.nslots * 256u + 2047u) / 2048u * 2048u;
     return std::min<uint32_t>(4u, (uint32_t)((160u * 1024u) / bytes));
 }
 
@@ -1856,7 +1857,7 @@ std::vector<StackPlan> more_waves(mk_net *h, SchedCache *sc, const SchedLimits &
 {
     std::vector<StackPlan> out;
     const JitLimits &jl = h->jit_lim;
-    if (!jl.lds_slot_bytes || jl.lds_quad) return out;
+    if (!jl.lds_slot_bytes) return out;
     JitLimits jl2 = jl;
     jl2.max_dops = std::max(jl.max_dops, kStackDops);
     // Each added register takes about one slot (an entry of the deepest
@@ -1911,7 +1912,7 @@ void use_plan(SchedCache *sc, StackPlan &&sp)
 void tune_lds_auto(mk_net *h, SchedCache *sc, const SchedLimits &lim0)
 {
     const JitLimits &jl = h->jit_lim;
-    auto bytes = [&](uint32_t n) { return ((uint64_t)jit_lds_words(n, jl.lds_quad) * 256u + 2047u) / 2048u * 2048u; };
+    auto bytes = [&](uint32_t n) { return ((uint64_t)n * 256u + 2047u) / 2048u * 2048u; };
     if (!heavy_stream(sc->prog, jl)) return;
     if (jl.lds_slot_bytes && bytes(sc->prog.nslots) * 4u <= 160u * 1024u) {
         // the knob's budget holds them at four waves per CU (C4 D=64: 41
@@ -3028,6 +3029,16 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint64_t resident = (uint64_t)jd.per_cu * (uint64_t)std::max(c.cus, 1);
         blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+        if (sc->jit.shape == JIT_MACHINE && nslots) {
+            // machine modules address a slot as slot x stride in 24-bit x 24-bit
+            // -> 32-bit arithmetic (module_prelude narrow_slots): stride
+            // (slot columns) < 2^24 and slots x stride < 2^32
+            const uint64_t per = sc->jit.pool >= 64 ? (uint64_t)sc->jit.pool  // slot columns per block (slot_cols below)
+                                 : sc->jit.pool ? block * sc->jit.pool : block;
+            const uint64_t cap = std::min<uint64_t>(((1ull << 32) - 1) / ((uint64_t)nslots * per), ((1ull << 24) - 1) / per);
+            if (cap < 1) return MK_ELIMIT;
+            blocks = (int)std::min<uint64_t>((uint64_t)blocks, cap);
+        }
         lanes = (uint64_t)blocks * block;
     }
     // stack-slot columns: one per thread, or (pool kernel) one per pool slot
@@ -3311,8 +3322,13 @@ struct SessK {
 
 // *queued (when given) is set once a kernel has been queued on `stream`, so
 // that a caller whose launch fails part way still orders later work after it.
+// `done` (when given) is recorded by the launch's last kernel itself, as its
+// completion event (hipExtModuleLaunchKernel / hipExtLaunchKernel stop
+// event), instead of by a separate hipEventRecord after it: that marker cost
+// ~3 us of stream time per call (round 6, profiles/r08_sessions_ab.txt).
 int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status, uint32_t *d_steps,
-                   hipStream_t stream, uint32_t ncalls = 1, bool resume = false, bool *queued = nullptr)
+                   hipStream_t stream, uint32_t ncalls = 1, bool resume = false, bool *queued = nullptr,
+                   hipEvent_t done = nullptr)
 {
     if (s->broken) return MK_EDEVICE;
     if (s->n == 0 || ncalls == 0) return MK_OK;
@@ -3334,8 +3350,11 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
         SessK k{s->n, ncalls, p.budget, d_in, d_out, d_status, d_steps, s->nsb, s->regs, s->slots,
                 s->hand_sb, s->hand_steps, s->hand_call, s->sflags, s->epoch};
         void *kargs[] = {(void *)&k};
-        if (hipModuleLaunchKernel(s->fn, (unsigned)blocks, 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr) !=
-            hipSuccess)
+        // the native kernel is the launch's last when the interpreter pass is
+        // skipped (below: no call can reach the budget)
+        const bool last = s->call_steps < (uint64_t)p.budget;
+        if (hipExtModuleLaunchKernel(s->fn, (uint32_t)(blocks * kBlock), 1, 1, kBlock, 1, 1, 0, stream, kargs, nullptr,
+                                     nullptr, last ? done : nullptr, 0) != hipSuccess)
             return MK_EDEVICE;
         if (queued) *queued = true;
         // 2. calls it handed off become interpreter sessions: imported by
@@ -3345,17 +3364,12 @@ int session_launch(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *
                            s->regs, s->slots, s->hdr, s->rec, s->dyn_base};
         // no call of this network can reach the budget: none hands off and
         // the interpreter holds no session, so its pass would only exit
-        // (MK_SESS_ALWAYS_INTERP=1 launches it anyway: A/B runs)
-        static const bool always = [] {
-            const char *e = std::getenv("MK_SESS_ALWAYS_INTERP");
-            return e && *e == '1';
-        }();
-        if (s->call_steps < (uint64_t)p.budget && !always) return MK_OK;
+        if (s->call_steps < (uint64_t)p.budget) return MK_OK;
     }
     // 3. the interpreter: its sessions (all of them without the native tier)
     void *args[] = {(void *)&code, (void *)&p};
-    if (hipLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)iblocks), dim3(kBlock), args, lds, stream) !=
-        hipSuccess) {
+    if (hipExtLaunchKernel(pick_session_kernel(s->nprog), dim3((unsigned)iblocks), dim3(kBlock), args, lds, stream,
+                           nullptr, done, 0) != hipSuccess) {
         if (s->native && !resume) s->broken = true;
         return MK_EDEVICE;
     }
@@ -3745,14 +3759,16 @@ int mk_session_compute_seq_device(mk_session *s, const int64_t *d_in, size_t nca
     // (reset, host calls) after this one
     if (int rc = mk::session_wait_last(s, st)) return rc;
     bool queued = false;
-    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls, false, &queued);
+    if (!s->order && hipEventCreateWithFlags(&s->order, hipEventDisableTiming) != hipSuccess) return MK_EDEVICE;
+    int rc = mk::session_launch(s, d_in, d_out, d_status, d_steps, st, (uint32_t)ncalls, false, &queued, s->order);
     if (rc) {
         // the native kernel may be running on `st` although the launch
         // failed after it: reset and teardown must still wait for it
         if (queued) (void)mk::session_mark(s, st);
         return rc;
     }
-    return mk::session_mark(s, st);
+    s->last = st; // the launch's last kernel recorded s->order (session_mark's event) on completion
+    return MK_OK;
 }
 
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,

@@ -994,21 +994,16 @@ void emit_stream_lane(const SchedProgram &p, const Graph &g, Emitter &e, const c
 // The guarded lane (MK_LANE_CHECKED) is for the CPU tests; the executor
 // gives launches with a smaller budget to tier 2.
 // Stream lanes with more than lim.heavy_ops micro-ops run in the heavy kernel.
-// How the heavy kernel reaches its LDS slots.  Volatile (JitLimits::
-// lds_volatile): every push is an LDS store and every pop an LDS load.
-// Otherwise LLVM may forward a store to the load that pops it and keep the
-// value in registers (nothing else touches the wave's LDS), which for deep
-// stacks turns into long chains of register moves (C4 D=256: 1,686 v_mov,
-// 132 VGPRs).
+// How the heavy kernel reaches its LDS slots: slot s of lane l at word
+// s * 64 + l.  LLVM may forward a store to the load that pops it and keep
+// the value in registers (nothing else touches the wave's LDS).  (Volatile
+// accesses and quad-interleaved slots were measured and lost: round 2-3,
+// DESIGN section 4b; removed in round 6.)
 void emit_lds_access(Emitter &e, const JitLimits &lim)
 {
-    e.line("#define MK_LDS_SLOTS %s", lim.lds_volatile ? "((volatile int32_t *)mk_lds_slots)" : "mk_lds_slots");
-    // word of slot s of this lane (JitLimits::lds_quad); the array holds
-    // whole quads: ceil(slots / 4) * 4 * 64 words
-    if (lim.lds_quad)
-        e.line("#define MK_LDS_IX(s) ((((uint32_t)(s) >> 2) * 64u + (threadIdx.x & 63u)) * 4u + ((uint32_t)(s) & 3u))");
-    else
-        e.line("#define MK_LDS_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
+    (void)lim;
+    e.line("#define MK_LDS_SLOTS mk_lds_slots");
+    e.line("#define MK_LDS_IX(s) ((uint32_t)(s) * 64u + (threadIdx.x & 63u))");
 }
 
 void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max_steps, bool checked)
@@ -1033,7 +1028,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         e.line("#define MK_SLOTS_BUFFER 1");
         e.line("#define MK_SLOTS_LDS_N %uu", nl);
         e.line("#define MK_HBM_NSLOTS (MK_NSLOTS - MK_SLOTS_LDS_N)");
-        e.line(g.lim->lds_quad ? "__shared__ int32_t mk_lds_slots[((MK_SLOTS_LDS_N + 3u) & ~3u) * 64u];" : "__shared__ int32_t mk_lds_slots[MK_SLOTS_LDS_N * 64u];");
+        e.line("__shared__ int32_t mk_lds_slots[MK_SLOTS_LDS_N * 64u];");
         emit_lds_access(e, *g.lim);
         e.line("MK_FN __amdgpu_buffer_rsrc_t mk_slot_rsrc(int32_t *b)");
         e.line("{");
@@ -1066,7 +1061,7 @@ void emit_stream(const SchedProgram &p, const Graph &g, Emitter &e, uint64_t max
         // No HBM traffic for the stacks.
         e.line("#ifndef MK_LANE_CHECKED");
         e.line("#define MK_SLOTS_LDS 1");
-        e.line(g.lim->lds_quad ? "__shared__ int32_t mk_lds_slots[((MK_NSLOTS + 3u) & ~3u) * 64u];" : "__shared__ int32_t mk_lds_slots[MK_NSLOTS * 64u];");
+        e.line("__shared__ int32_t mk_lds_slots[MK_NSLOTS * 64u];");
         emit_lds_access(e, *g.lim);
         e.line("#define MK_SLOT_IX(s) MK_LDS_IX(s)");
         e.line("#undef MK_SLOT_ST");
@@ -1315,7 +1310,6 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     // iterations than uf chunks alone (a 2 uf chunk starts only when a lane
     // needs over uf of them).  MK_JIT_SAT_TIER=0: uf chunks only.
     auto emit_sat_tier = [&](const char *c) {
-        if (!g.lim->sat_tier) return;
         e.line("    while (more && T32 - it >= %uu && MK_KEEP(%s > %d, need)) {", 2 * uf, c, uf);
         e.line("    it += %uu;", 2 * uf);
         if (uf % (int)g.lim->sat_block == 0)
@@ -1340,7 +1334,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     e.line("        break;");
     e.line("    }");
     e.line("    const uint32_t need = MK_LOOP_NEED(pol);");
-    if (g.lim->prio) e.line("    MK_PRIO_LOOP();");
+    e.line("    MK_PRIO_LOOP();");
     e.line("    bool a = true, more = true;");
     if (ovf) {
         e.line("    bool ovf_ = false, brx_ = false;");
@@ -1456,7 +1450,7 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     for (int u = 0; u < kLoopUnroll; ++u) iteration(LOOP_GUARDED);
     e.line("    } while (MK_KEEP(a, need));");
     e.line("    }");
-    if (g.lim->prio) e.line("    MK_PRIO_REST();");
+    e.line("    MK_PRIO_REST();");
     // a: still in the loop (suspended); otherwise it left through the branch
     // (the condition on its frozen registers fails) or through the guard
     if (brx) {
@@ -1494,7 +1488,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     std::vector<uint32_t> loops;
     e.line("// generated from a compiled schedule: %zu variants reachable, %zu micro-ops, cyclic", g.nreach, g.ndops);
     e.line("#define MK_JIT_MACHINE 1");
-    if (g.lim->prio) { // wave priority around self-loops (MK_JIT_PRIO, the module header); none in host builds
+    { // wave priority around self-loops (the module header); none in host builds
         e.line("#ifndef MK_PRIO_LOOP");
         e.line("#define MK_PRIO_LOOP()");
         e.line("#define MK_PRIO_REST()");
@@ -1612,7 +1606,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     // so the scalar switch from 32 reachable variants (MK_JIT_UNIFORM_SW=1|0
     // forces either).
     {
-        const bool scalar = g.lim->uniform_sw == 1 || (g.lim->uniform_sw < 0 && g.nreach >= 32);
+        const bool scalar = g.nreach >= 32;
         e.line(scalar ? "#define MK_SCALAR(u) mk_scalar(u)" : "#define MK_SCALAR(u) (u)");
     }
     const size_t fn_start = e.s.size();
@@ -1781,7 +1775,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
             body_range(g, v, lo, hi);
             return !round_ends(g, v, lo, hi).segs.empty() && !has_inline_exit(g, lo, hi);
         };
-        bool split = g.lim->sweep_cold;
+        bool split = true;
         for (uint32_t v : fo) split = split && (!checked(v) || v < 64u);
         std::string l = "#define MK_SWEEP_LIST(X)", c = "#define MK_SWEEP_COLD(X)";
         uint64_t mask = 0;
@@ -1829,7 +1823,7 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
 uint32_t jit_lds_slot_count(uint32_t nslots, bool heavy, const JitLimits &lim)
 {
     if (jit_slots_in_lds(nslots, heavy, lim)) return nslots;
-    if (!lim.lds_split || !heavy || !nslots || lim.slot_layout == 0 || lim.slot_nt) return 0;
+    if (!lim.lds_split || !heavy || !nslots || lim.slot_layout == 0) return 0;
     if (lim.slot_layout < 0 && nslots > kJitWaveBlockedSlots) return 0; // lane-major layout: no split
     // as many slots as fit the LDS budget in 2 KiB allocation granules
     const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
@@ -1844,7 +1838,7 @@ bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim)
 {
     // one workgroup may hold at most the CU's 160 KiB of LDS
     const uint64_t cap = std::min<uint64_t>(lim.lds_slot_bytes, 160u * 1024u);
-    return heavy && nslots && lim.slot_layout != 0 && !lim.slot_nt && (uint64_t)jit_lds_words(nslots, lim.lds_quad) * 256u <= cap;
+    return heavy && nslots && lim.slot_layout != 0 && (uint64_t)nslots * 256u <= cap;
 }
 
 bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &src, std::string &why, JitShape *shape,
@@ -1873,7 +1867,7 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
     if (s == JIT_MACHINE) {
         emit_machine_lane(p, g, e);
     } else {
-        if (lim.narrow) narrow_regs(g);
+        narrow_regs(g);
         emit_stream(p, g, e, max_fast_steps(p, g), checked);
     }
     if (!checked && e.s.size() > lim.max_src_bytes) {
@@ -2353,8 +2347,6 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_HEAVY_OPS", l.heavy_ops);
     num("MK_JIT_SLOT_BYTES", l.slot_bytes);
     if (!l.slot_bytes) l.slot_bytes = kJitSlotBytes;
-    flag("MK_JIT_SLOT_NT", l.slot_nt);
-    flag("MK_JIT_IO_NT", l.io_nt);
     num("MK_JIT_POOL", l.pool);
     flag("MK_JIT_ORDER", l.order);
     flag("MK_JIT_TILE_SORT", l.tile_sort);
@@ -2368,18 +2360,10 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_VGPR_FILE", l.vgpr_file);
     if (!l.vgpr_file || l.vgpr_file > 512) l.vgpr_file = 512;
     flag("MK_JIT_SWEEP", l.sweep);
-    flag("MK_JIT_SWEEP_COLD", l.sweep_cold);
-    num("MK_JIT_SWEEP_PASSES", l.sweep_passes);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
-    flag("MK_JIT_LDS_VOLATILE", l.lds_volatile);
-    flag("MK_JIT_NARROW", l.narrow);
-    flag("MK_JIT_LDS_QUAD", l.lds_quad);
-    if (const char *v = std::getenv("MK_JIT_UNIFORM_SW"); v && *v) l.uniform_sw = v[0] == '1' ? 1 : v[0] == '0' ? 0 : -1;
     flag("MK_JIT_PROF", l.prof);
-    flag("MK_JIT_PRIO", l.prio);
-    flag("MK_JIT_SAT_TIER", l.sat_tier);
     if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
     return l;
 }
@@ -2388,21 +2372,16 @@ std::string JitLimits::key() const
 {
     char b[256];
     snprintf(b, sizeof b,
-             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,nt=%d%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
-             "tsort=%d,tsr=%u,lds=%zu%s,tune=%d,split=%u,ldsv=%d,nar=%d,quad=%d,sblk=%u",
+             "shape=%s,policy=%08x,dops=%zu,src=%zu,unroll=%d,layout=%d,pf=%zu,heavy=%zu,pool=%u,order=%d,"
+             "tsort=%d,tsr=%u,lds=%zu%s,tune=%d,split=%u,sblk=%u",
              force_machine ? "machine" : force_stream ? "stream" : "auto", policy, max_dops, max_src_bytes,
-             loop_unroll, slot_layout, (int)slot_nt, (int)io_nt, prefetch, heavy_ops, pool, (int)order,
+             loop_unroll, slot_layout, prefetch, heavy_ops, pool, (int)order,
              (int)tile_sort, ts_rounds, lds_slot_bytes, lds_auto ? "auto" : "",
-             (int)tune_regs, lds_split, (int)lds_volatile, (int)narrow, (int)lds_quad, sat_block);
+             (int)tune_regs, lds_split, sat_block);
     std::string k = b;
     if (!sat_count) k += ",scount=0";
     if (!sweep) k += ",sweep=0";
-    if (!sweep_cold) k += ",scold=0";
-    if (sweep_passes != 1) k += ",spass=" + std::to_string(sweep_passes);
-    if (uniform_sw >= 0) k += uniform_sw ? ",usw=1" : ",usw=0";
     if (prof) k += ",prof=1";
-    if (!prio) k += ",prio=0";
-    if (!sat_tier) k += ",stier=0";
     if (vgpr_file != 512) k += ",vfile=" + std::to_string(vgpr_file);
     return k;
 }
@@ -2695,7 +2674,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 namespace {
 // Everything a module needs before its lane code: types, status codes,
 // policy, the flag / loop helpers, the slot-access macros, mk_device_common.
-std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, bool sat)
+std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, bool sat, bool narrow_slots = false)
 {
     Emitter e;
     if (shape == JIT_MACHINE && pool >= 64) e.line("#define MK_POOL %uu", pool);
@@ -2731,7 +2710,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     if (lim.ts_rounds) // kMachineSortKernel: lanes per thread per tile (else the lane source's choice)
         e.line("#define MK_TS_R %uu", lim.ts_rounds);
     if (shape == JIT_MACHINE) // machine kernels: sweep passes before rounds (stream modules' sources as they were)
-        e.line("#define MK_SWEEP_PASSES %uu", lim.sweep_passes);
+        e.line("#define MK_SWEEP_PASSES 1u");
     if (lim.prof) { // kMachineSortKernel: cycles per phase in place of the counters (MK_JIT_PROF)
         e.line("#define MK_PROF 1");
         e.line("#define MK_T() __builtin_amdgcn_s_memtime()");
@@ -2741,7 +2720,7 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
     // loop (dispatch rounds, latency-bound) at 1, so the issue arbiter
     // prefers them over the loops' throughput-bound VALU streams (a wave
     // starts at 0)
-    if (lim.prio && shape == JIT_MACHINE) {
+    if (shape == JIT_MACHINE) {
         e.line("#define MK_PRIO_LOOP() __builtin_amdgcn_s_setprio(0)");
         e.line("#define MK_PRIO_REST() __builtin_amdgcn_s_setprio(1)");
     }
@@ -2785,23 +2764,25 @@ std::string module_prelude(JitShape shape, const JitLimits &lim, uint32_t pool, 
         e.s += b;
         e.line("#define MK_SATDECB(x) mk_satdecb(x)");
     }
-    // stack-slot accesses (MK_JIT_SLOT_NT=1: non-temporal, experiments)
-    if (lim.slot_nt) {
-        e.line("#define MK_SLOT_ST(b, ss, s, v) __builtin_nontemporal_store((v), (b) + (uint64_t)(s) * (ss))");
-        e.line("#define MK_SLOT_LD(b, ss, s) __builtin_nontemporal_load((b) + (uint64_t)(s) * (ss))");
+    // stack-slot accesses
+    e.line("#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))");
+    e.line("#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])");
+    // per-lane slot numbers (dynamic stacks); the buffer-op form redefines them.
+    // Machine kernels (narrow_slots): slot x stride in one full-rate 24-bit
+    // multiply (v_mul_u32_u24) instead of a 64 x 64-bit product (two
+    // v_mad_u64_u32 and moves per access); the executor keeps stride < 2^24
+    // and slots x stride < 2^32 (launch_jit_locked).
+    if (narrow_slots) {
+        e.line("extern \"C\" __device__ uint32_t __ockl_mul24_u32(uint32_t, uint32_t);");
+        e.line("#define MK_SLOT_STX(b, ss, s, v) ((b)[__ockl_mul24_u32((uint32_t)(s), (uint32_t)(ss))] = (v))");
+        e.line("#define MK_SLOT_LDX(b, ss, s) ((b)[__ockl_mul24_u32((uint32_t)(s), (uint32_t)(ss))])");
     } else {
-        e.line("#define MK_SLOT_ST(b, ss, s, v) ((b)[(uint64_t)(s) * (ss)] = (v))");
-        e.line("#define MK_SLOT_LD(b, ss, s) ((b)[(uint64_t)(s) * (ss)])");
+        e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
+        e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
     }
-    // per-lane slot numbers (dynamic stacks); the buffer-op form redefines them
-    e.line("#define MK_SLOT_STX(b, ss, s, v) MK_SLOT_ST(b, ss, s, v)");
-    e.line("#define MK_SLOT_LDX(b, ss, s) MK_SLOT_LD(b, ss, s)");
-    // vector out/status stores of the light stream kernel (MK_JIT_IO_NT=1: non-temporal, experiments)
+    // vector out/status stores of the light stream kernel
     e.line("typedef int32_t mk_i32x4 __attribute__((ext_vector_type(4)));");
-    if (lim.io_nt)
-        e.line("#define MK_IO_ST(ptr, v) __builtin_nontemporal_store((v), (ptr))");
-    else
-        e.line("#define MK_IO_ST(ptr, v) (*(ptr) = (v))");
+    e.line("#define MK_IO_ST(ptr, v) (*(ptr) = (v))");
     // loop policy of the machine shape (see kMachineKernel)
     e.line("MK_FN uint32_t mk_loop_need(uint32_t pol)");
     e.line("{");
@@ -2922,7 +2903,7 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
                               uint32_t pool)
 {
     Emitter e;
-    e.s = module_prelude(shape, lim, pool, lane_src.find("MK_SAT") != std::string::npos);
+    e.s = module_prelude(shape, lim, pool, lane_src.find("MK_SAT") != std::string::npos, shape == JIT_MACHINE);
     e.s += lane_src;
     const char *mk = lim.tile_sort && !lim.order ? kMachineSortKernel
                                                  : kMachineKernel;

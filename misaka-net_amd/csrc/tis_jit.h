@@ -75,8 +75,6 @@ struct JitLimits {
     uint32_t policy = kJitPolicy;          // MK_JIT_POLICY=refill,num,min
     int loop_unroll = 0;                   // MK_JIT_LOOP_UNROLL (0: by body size, fast_unroll)
     int slot_layout = -1;                  // MK_JIT_SLOT_LAYOUT=blocked(1)|lane(0); -1: by size
-    bool slot_nt = false;                  // MK_JIT_SLOT_NT=1: non-temporal slot accesses
-    bool io_nt = false;                    // MK_JIT_IO_NT=1: non-temporal out/status stores
     size_t prefetch = kJitPrefetchLoads;   // MK_JIT_PREFETCH (0: off)
     size_t heavy_ops = kJitHeavyOps;       // MK_JIT_HEAVY_OPS
     uint64_t slot_bytes = kJitSlotBytes;   // MK_JIT_SLOT_BYTES
@@ -106,18 +104,11 @@ struct JitLimits {
     // lanes without stack slots, 4 with them -- r02ak: C5 212-214 vs 215 us
     // but the JRO-heavy census class 58.9 vs 52.1 ms, so not the default.
     uint32_t ts_rounds = 4;
-    // Stream shape: registers whose high 32 bits nothing reads are computed
-    // in 32 bits (narrow_regs in tis_jit.cpp; MK_JIT_NARROW=0: all int64).
-    bool narrow = true;
     // kMachineSortKernel dispatches by sweeps over the variants in reverse
     // postorder (tis_jit.cpp forward_order), each variant one ballot when no
     // lane is on it, instead of one variant per round (MK_JIT_SWEEP=0: rounds;
     // C5 105.8 -> 97.0 us, profiles/r06u_c5_sweep_ab.txt).
     bool sweep = true;
-    // the sweep's checked variants last, behind one ballot (MK_JIT_SWEEP_COLD=0: in order)
-    bool sweep_cold = true;
-    // sweep passes before the round dispatcher takes the lanes left (MK_JIT_SWEEP_PASSES)
-    uint32_t sweep_passes = 1;
     // Heavy stream kernel: a lane's stack slots live in LDS instead of HBM
     // when the wave's nslots x 256 B fit this many bytes (MK_JIT_LDS_SLOTS,
     // 0 = never).  One 64-thread block per wave, so the bound also sets the
@@ -147,36 +138,11 @@ struct JitLimits {
     // first lds_slot_bytes / 256 of them in LDS and the rest in HBM, when
     // that is at least this percentage of them (MK_JIT_LDS_SPLIT; 0: HBM only).
     uint32_t lds_split = 75;
-    // LDS slot accesses as volatile (MK_JIT_LDS_VOLATILE): LLVM keeps every
-    // push and pop in LDS instead of forwarding stores to loads in registers.
-    bool lds_volatile = false;
-    // LDS slots interleaved in quads (MK_JIT_LDS_QUAD): slot s of lane l at
-    // word ((s / 4) * 64 + l) * 4 + s % 4, so four consecutive slots of a lane
-    // are one 16-byte word and LLVM merges a stack's consecutive pushes and
-    // pops into ds_write_b128 / ds_read_b128 (twice the LDS bytes per clock of
-    // b32 accesses).  Off (default): slot s at s * 64 + l.  Measured r03f:
-    // C4 D=64 47.6 us with quads vs 24.2 without, D=256 159.5 vs 161.8.
-    bool lds_quad = false;
-    // Machine lanes switch on a wave-uniform scalar (MK_SCALAR: the
-    // dispatched variant through an empty SGPR asm) or on the plain value,
-    // which LLVM's GVN swaps for the lane's own superblock id and lowers as
-    // a divergent compare tree (round 4; emit_machine_lane).  -1: scalar
-    // from 32 reachable variants; MK_JIT_UNIFORM_SW=1|0 forces either.
-    int uniform_sw = -1;
     // Diagnostics: the tile-sorted machine kernel reports shader-clock cycles
     // per phase (sort, chunks, loop and other variants, results) and its
     // dispatch rounds in place of the launch's counters (MK_JIT_PROF=1;
     // tools/probe/c5_decomp.py).  The launch's statistics are then not counts.
     bool prof = false;
-    // Wave priority: 0 inside self-loops, 1 after them (module_prelude;
-    // MK_JIT_PRIO=0: none).  The issue arbiter then prefers the dispatch
-    // rounds' latency-bound waves over the loops' VALU streams (r05o, C5
-    // launch 120.6 / 121.1 -> 111.7 / 111.6 us).
-    bool prio = true;
-    // Saturating countdowns run chunks of twice the unroll while some lane
-    // still needs more than one unroll (emit_self_loop; MK_JIT_SAT_TIER=0: off).
-    // C5 111.1 / 111.6 -> 105.3 / 105.3 us (r05s); GPU parity subset green with it.
-    bool sat_tier = true;
 
     // VGPRs per SIMD lane a module's waves share when a stack plan's module
     // is checked against its waves per SIMD (mk_exec.hip module_holds):
@@ -212,8 +178,6 @@ bool jit_lane_source(const SchedProgram &p, const JitLimits &lim, std::string &s
 
 // Whether the heavy stream kernel keeps the lane's `nslots` stack slots in
 // LDS (the executor then allocates no HBM slots and launches one grid).
-// LDS words per lane for n slots: whole quads (JitLimits::lds_quad)
-inline uint32_t jit_lds_words(uint32_t n, bool quad) { return quad ? (n + 3u) & ~3u : n; }
 bool jit_slots_in_lds(uint32_t nslots, bool heavy, const JitLimits &lim);
 // Slots of the lane the heavy stream kernel keeps in LDS: all (jit_slots_in_lds),
 // the first ones with JitLimits::lds_split, or none.

@@ -397,7 +397,6 @@ class Compiler {
     void exit_end(uint8_t reason);
     void exit_branch(int n, uint8_t cond, uint16_t target);
     void exit_jro(int n, const Val &v);
-    void exit_pop_check(int s);
     bool inline_pop_check(int s);
     void round_end_marker();
     void generalize();
@@ -862,25 +861,6 @@ bool Compiler::inline_pop_check(int s)
     return true;
 }
 
-// POP from a dynamic stack whose memory part may be empty: branch on DEP.
-// Both successors re-attempt the POP (same node, same round position): the
-// taken one knows DEP == 0 (the constant: the POP blocks), the other DEP >= 1.
-void Compiler::exit_pop_check(int s)
-{
-    Ctl t = ctl_, f = ctl_;
-    f.lo[s] = 1;
-    std::vector<Ctl> succ{t, f};
-    std::vector<std::vector<Val>> sl;
-    const Val a = canonicalize(succ, sl, loc_[DEP(s)]);
-    if (fail_) return;
-    sl[0][DEP(s)] = vconst(0);
-    const uint32_t it = get_or_create(succ[0], sl[0]);
-    const uint32_t iff = get_or_create(succ[1], sl[1]);
-    const int64_t imm = (int64_t)(((uint64_t)(2 * iff) << 32) | (uint64_t)(2 * it));
-    emit(U_BR, (uint8_t)(fa(a) | (0 << UF_COND_SHIFT)), 0, a.r, 0, imm);
-    emit_ext(steps_);
-}
-
 void Compiler::round_end_marker()
 {
     const Val o = out_val();
@@ -1024,10 +1004,6 @@ int Compiler::attempt(int n)
             const Val D = loc_[DEP(s)];
             if (D.kind == K_CONST && D.c == 0) return A_CONT;
             if (D.kind == K_REG && ctl_.lo[s] == 0) {
-                if (!lim_.side_exits) {
-                    exit_pop_check(s);
-                    return A_EXIT;
-                }
                 if (!inline_pop_check(s)) return A_EXIT;
             }
             const Val D2 = loc_[DEP(s)]; // in its home now
@@ -1572,7 +1548,6 @@ SchedLimits lim_env(SchedLimits lim)
     if (const char *e = getenv("MK_SCHED_WIDEN")) lim.widen_after = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_DYN")) lim.dyn_depths = (uint32_t)atoi(e);
     if (const char *e = getenv("MK_SCHED_MAX_SB")) lim.max_superblocks = (uint32_t)atoi(e);
-    if (const char *e = getenv("MK_SCHED_SIDE_EXITS")) lim.side_exits = atoi(e) != 0;
     if (const char *e = getenv("MK_SCHED_SHARE")) lim.share_slots = atoi(e) != 0;
     if (const char *e = getenv("MK_SCHED_MAX_REGS")) {
         const int v = atoi(e);

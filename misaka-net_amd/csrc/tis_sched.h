@@ -78,7 +78,6 @@ struct SchedLimits {
     uint64_t max_rounds = 1ull << 22;      // symbolic rounds in total (compile-time bound)
     uint32_t dyn_depths = 24;              // distinct entry depths before a stack turns dynamic (0 = never)
     uint32_t widen_after = 2;              // states of one shape with other constants before widening (0 = never)
-    bool side_exits = true;                // dynamic POP checks as in-line side exits (BRX), else branch exits
     bool share_slots = true;               // acyclic graphs: stacks never in use together share slots
 };
 
