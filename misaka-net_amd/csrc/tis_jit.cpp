@@ -1220,10 +1220,15 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
     bool ovf = false;
     for (size_t pc = gpc + 1; pc < xpc; ++pc) ovf = ovf || g.D[pc].op == U_OVF || g.D[pc].op == U_BRX;
     const DOp *brx = g.D[gpc + 1].op == U_BRX ? &g.D[gpc + 1] : nullptr;
-    // induction register: written once per iteration, by r += imm (no truncation)
+    // induction register: written once per iteration, by r += imm (no
+    // truncation).  Loops with an OVF / BRX exit have one too since round 6
+    // (a dynamic PUSH loop's depth register): the exit drops the lane's flag
+    // before the bump, so the bumps count exactly the iterations completed,
+    // as the per-lane counter did; the register then needs no select and
+    // runs in 32 bits in the narrow phase (t2_dyn_depth 130 -> ? us).
     int ind = -1;
     int64_t step = 0;
-    for (size_t pc = gpc + 1; pc < xpc && ind < 0 && !ovf; ++pc) {
+    for (size_t pc = gpc + 1; pc < xpc && ind < 0; ++pc) {
         const DOp &I = g.D[pc];
         if (I.op == U_ADDI && I.a == I.d && !(I.fl & UF_TA) && nwr[I.d / 8] == 1 && I.imm != 0 &&
             I.imm > -(int64_t(1) << 31) && I.imm < (int64_t(1) << 31))
@@ -2141,6 +2146,9 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
     // wave-uniform (scalar registers): outputs, lanes, and the four end reasons
     uint64_t c_steps = 0u;
     uint32_t c_out = 0u, c_done = 0u, c_qu = 0u, c_bu = 0u, c_ov = 0u, c_os = 0u;
+    // stack slots lane-major ([slot][lanes]: a slot row of all resident
+    // lanes is contiguous; wave-blocked rows measured slower here, round 6:
+    // t1_two_stacks 236 -> 266 us, t2_dyn_depth 120 -> 123 us, r08n)
     int32_t *slots = p.slots ? p.slots + gid : (int32_t *)0;
 #if MK_PROF
     // MK_JIT_PROF: shader-clock cycles per phase, per wave, in place of the
