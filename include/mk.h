@@ -206,7 +206,9 @@ int mk_session_compute_seq(mk_session *s, const int64_t *in, size_t ncalls, int3
  * own stream); calls on one session are ordered device-side, with no host
  * synchronisation: a call waits on an event recorded after the previous
  * launch when that ran on another stream (calls on one stream follow stream
- * order), and the session's synchronous calls below wait on it too.  A
+ * order), and the session's synchronous calls below wait on it too.  The
+ * event is the completion event of the launch's last kernel (no separate
+ * marker on the stream: ~3 us per call less).  A
  * caller stream must outlive the session work queued on it; mk_session_free
  * waits for the last launch on any stream. */
 int mk_session_compute_device(mk_session *s, const int64_t *d_in, int32_t *d_out, uint8_t *d_status,
