@@ -1810,6 +1810,10 @@ void emit_machine_lane(const SchedProgram &p, const Graph &g, Emitter &e)
     }
     e.line("}");
     if (p.session) return; // sessions: mk_sess_exec drives mk_run; no single-lane form
+    // two lanes per thread in the tile-sorted kernel (MK_JIT_PAIR): one
+    // sweep pass for two chunks; two lanes would share the thread's slot
+    // column, and the phase profile (MK_JIT_PROF) times the one-lane form
+    if (g.lim->pair && !p.nslots && g.lim->ts_rounds % 2u == 0u && !g.lim->prof) e.line("#define MK_PAIR 1");
     // the whole lane, for the CPU tests (the kernel drives mk_run itself)
     e.line("MK_FN int32_t mk_lane(int64_t in, uint32_t budget, int32_t *__restrict__ slots, uint64_t sstride,");
     e.line("                      uint32_t *steps_out, uint32_t *status_out)");
@@ -2229,6 +2233,73 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 #endif
         // 2. the sorted lanes, 64 per chunk, each wave's chunks in snake order
         // (the next tile's first barrier keeps s_kp until every wave is done)
+#if defined(MK_PAIR)
+        // two lanes per thread: a pair of adjacent sorted chunks, the pairs
+        // in snake order.  One sweep pass serves both lanes (a variant's
+        // ballot, its skip when neither lane is on it); the loops still run
+        // one lane at a time: a paired countdown (two interleaved dependency
+        // chains, measured round 6) did 6% more decrements, 2 x max(A, B)
+        // against A + B, without a faster rate (profiles/r08_c5_sort_ab.txt)
+        for (uint32_t r = 0; r < MK_TS_R; r += 2u) {
+            const uint32_t q = (r >> 1) * 4u + (((r >> 1) & 1u) ? 3u - wave : wave);
+            const uint32_t jA = q * 128u + lane, jB = jA + 64u;
+            const bool liveA = jA < m, liveB = jB < m;
+            uint64_t kpA = liveA ? s_kp[jA] : 0u;
+            const uint64_t kpB = liveB ? s_kp[jB] : 0u;
+            MkLane A, B;
+            mk_init(A, (int32_t)(uint32_t)kpA);
+            mk_init(B, (int32_t)(uint32_t)kpB);
+            if (!liveA) A.sb = MK_SB_IDLE;
+            if (!liveB) B.sb = MK_SB_IDLE;
+#if defined(MK_SWEEP_LIST)
+#define MK_SWEEP_STEP(v, loop)                                                                   \
+            if (__ballot(A.sb == (v) || B.sb == (v))) {                                              \
+                const uint32_t smA_ = (loop) ? MK_WAVE_MAX(A.sb == (v) ? A.steps : 0u) : 0u;         \
+                if (A.sb == (v)) mk_run((v), A, p.budget, slots, p.lanes, pol, smA_);                \
+                const uint32_t smB_ = (loop) ? MK_WAVE_MAX(B.sb == (v) ? B.steps : 0u) : 0u;         \
+                if (B.sb == (v)) mk_run((v), B, p.budget, slots, p.lanes, pol, smB_);                \
+            }
+            MK_SWEEP_LIST(MK_SWEEP_STEP)
+#if defined(MK_SWEEP_COLD)
+            if (__ballot((A.sb < 64u && ((MK_SWEEP_COLD_MASK >> A.sb) & 1ull)) ||
+                         (B.sb < 64u && ((MK_SWEEP_COLD_MASK >> B.sb) & 1ull)))) {
+                MK_SWEEP_COLD(MK_SWEEP_STEP)
+            }
+#endif
+#undef MK_SWEEP_STEP
+#endif
+            // what the pass left, lane A then lane B (B moved into A): rounds
+            bool live = liveA;
+#pragma unroll 1
+            for (uint32_t h = 0; h < 2u; ++h) {
+                for (;;) {
+                    const unsigned long long actb = __ballot(A.sb < MK_SB_DONE);
+                    if (!actb) break;
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)A.sb, (int)__builtin_ctzll(actb));
+                    const uint32_t smax = mk_is_loop(u) ? MK_WAVE_MAX(A.sb == u ? A.steps : 0u) : 0u;
+                    const uint32_t us = MK_SCALAR(u);
+                    if (A.sb == u) mk_run(us, A, p.budget, slots, p.lanes, pol, smax);
+                }
+                if (live) {
+                    const uint64_t at = base + (kpA >> 32);
+                    p.out[at] = (A.st & MK_ST_HAS_OUTPUT) ? A.outv : 0;
+                    p.status[at] = (uint8_t)A.st;
+                    if (p.steps) p.steps[at] = A.steps;
+                }
+                const uint32_t rs = live ? (A.st & MK_ST_REASON_MASK) : 0u;
+                c_steps += live ? (uint64_t)A.steps : 0u;
+                c_out += (uint32_t)__popcll(__ballot(live && (A.st & MK_ST_HAS_OUTPUT)));
+                c_done += (uint32_t)__popcll(__ballot(live));
+                c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
+                c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
+                c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
+                c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
+                A = B;
+                kpA = kpB;
+                live = liveB;
+            }
+        }
+#else
         for (uint32_t r = 0; r < MK_TS_R; ++r) {
             const uint32_t c = r * 4u + ((r & 1u) ? 3u - wave : wave);
             const uint32_t j = c * 64u + lane;
@@ -2290,6 +2361,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
             c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
         }
+#endif
 #if MK_PROF
         pf_chunk += MK_T() - pf_a;
 #endif
@@ -2366,6 +2438,7 @@ JitLimits JitLimits::from_env()
     num("MK_JIT_SAT_BLOCK", l.sat_block);
     if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
     num("MK_JIT_VGPR_FILE", l.vgpr_file);
+    flag("MK_JIT_PAIR", l.pair);
     if (!l.vgpr_file || l.vgpr_file > 512) l.vgpr_file = 512;
     flag("MK_JIT_SWEEP", l.sweep);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
@@ -2391,6 +2464,7 @@ std::string JitLimits::key() const
     if (!sweep) k += ",sweep=0";
     if (prof) k += ",prof=1";
     if (vgpr_file != 512) k += ",vfile=" + std::to_string(vgpr_file);
+    if (!pair) k += ",pair=0";
     return k;
 }
 

@@ -130,6 +130,10 @@ struct JitLimits {
     // as one saturating decrement of its remaining-iteration count per
     // iteration (MK_JIT_SAT_COUNT=0: the bump and a med3 / shift flag).
     bool sat_count = true;
+    // Two lanes per thread in the tile-sorted kernel when the network has no
+    // stack slots: one sweep pass for two sorted chunks (MK_PAIR in
+    // kMachineSortKernel; MK_JIT_PAIR=0: one lane per thread).
+    bool pair = true;
     // Heavy stream networks whose LDS slots allow fewer than four waves per
     // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
     // mk_exec.hip tune_soft_regs).

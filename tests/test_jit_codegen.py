@@ -135,6 +135,21 @@ def test_wide_immediates_and_stop(tmp_path, machine):
     assert len(check_cases(tmp_path, cases, machine)) == 3
 
 
+def test_paired_dispatch_marker(monkeypatch):
+    # Two lanes per thread in the tile-sorted kernel (round 6, MK_PAIR in
+    # kMachineSortKernel): networks without stack slots, one sweep pass for
+    # two sorted chunks; the lanes' own code is the one-lane form, so every
+    # machine-shape parity test here and on the GPU covers it.  Stack slots
+    # (one column per thread) and MK_JIT_PAIR=0 keep one lane per thread.
+    src, ns = sc.jit_lane(mk.networks.countdown_network(), machine=True)
+    assert ns == 0 and "#define MK_PAIR 1" in src
+    src, ns = sc.jit_lane(mk.networks.pipeline_network(64), machine=True)
+    assert ns > 0 and "#define MK_PAIR 1" not in src
+    monkeypatch.setenv("MK_JIT_PAIR", "0")
+    src, _ = sc.jit_lane(mk.networks.countdown_network(), machine=True)
+    assert "#define MK_PAIR 1" not in src
+
+
 def test_loop_phases(tmp_path):
     # every path of the machine shape's self-loops (tisgen.loop_cases)
     cases = [(lbl, nodes, np.asarray(xs, np.int64), kw) for lbl, nodes, xs, kw in loop_cases()]
