@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/$1; shift; mkdir -p $OUT; export TMPDIR=/tmp
 for pass in 1 2; do
- for m in 1023 0; do
+ for m in ${C5_MASKS:-1023 0}; do
   for set in "$@"; do
    lab=${set%%:*}; envs=${set#*:}
    env $envs timeout -k 10 120 python -u tools/probe/c5_decomp.py $m 4194304 20 \
