@@ -1517,10 +1517,28 @@ struct SchedDev {
 };
 
 // Tier 3: the schedule compiled to a native kernel (tis_jit.h).
+// Grid of the tile-sorted machine kernel for networks with stack slots in
+// HBM, measured (launch_jit_locked): the first launches at a batch size run
+// the resident grid and two smaller ones (3/4, 1/2 of its blocks), each
+// bracketed by events; the first launch after all three have completed
+// (hipEventQuery, never waiting) keeps the fastest.  Slot-heavy kernels split
+// on it: t1_two_stacks (1 KiB of stores per lane) runs 233 -> 192 us at 3/4
+// of the blocks, t2_dyn_depth (pushes read back) 119 -> 138 us
+// (profiles/r08_grid_tune_ab.txt).  Results do not depend on the grid.
+struct GridTune {
+    uint64_t n = 0;          // batch size the state is for (another size starts over)
+    int phase = 0;           // 0..2: candidate `phase` launched next; 3: deciding; 4: decided
+    int cand[3] = {0, 0, 0}; // blocks: 3/4, 1/2, all of the resident grid (cold launch first)
+    int chosen = 0;
+    float ms[3] = {0, 0, 0};
+    hipEvent_t ev[6] = {};
+};
+
 struct JitDev {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     int per_cu = 0;
+    GridTune tune;
 };
 
 struct JitState {
@@ -1678,6 +1696,8 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_order);
                 (void)hipFree(sc->dev[d].d_ordtab);
                 mk::release_module(sc->jit.dev[d].mod, sc->jit.rtc);
+                for (hipEvent_t e : sc->jit.dev[d].tune.ev)
+                    if (e) (void)hipEventDestroy(e);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
             if (c.ev) (void)hipEventDestroy(c.ev);
@@ -2991,6 +3011,53 @@ uint64_t host_chunk_from_env()
     return x ? (uint64_t)x : (uint64_t)1 << 22;
 }
 
+// GridTune: batches from this size on are tuned (smaller ones run the
+// resident grid; their launches are short and their grid often not full)
+constexpr uint64_t kGridTuneMin = uint64_t(1) << 18;
+
+struct GridPick {
+    int blocks = 0;
+    int timed = -1; // candidate whose events bracket this launch, or -1
+};
+
+// One launch's grid under GridTune (`resident`: the untuned grid).
+GridPick grid_tune_pick(GridTune &t, uint64_t n, int resident)
+{
+    GridPick g;
+    g.blocks = resident;
+    if (t.n != n || t.cand[2] != resident) {
+        t.n = n;
+        t.phase = 0;
+        t.cand[0] = std::max(1, resident * 3 / 4);
+        t.cand[1] = std::max(1, resident / 2);
+        t.cand[2] = resident;
+        t.chosen = resident;
+    }
+    if (t.phase < 3) {
+        for (hipEvent_t &e : t.ev)
+            if (!e && hipEventCreate(&e) != hipSuccess) {
+                t.phase = 4; // no events: the resident grid
+                return g;
+            }
+        g.timed = t.phase;
+        g.blocks = t.cand[t.phase++];
+        return g;
+    }
+    if (t.phase == 3) {
+        if (hipEventQuery(t.ev[5]) != hipSuccess) return g; // not measured yet: never wait
+        bool ok = true;
+        for (int k = 0; k < 3; k++) ok = ok && hipEventElapsedTime(&t.ms[k], t.ev[2 * k], t.ev[2 * k + 1]) == hipSuccess;
+        // a smaller grid is kept only when it is clearly faster (5%)
+        int best = 2;
+        for (int k = 0; k < 2; k++)
+            if (ok && t.ms[k] > 0.f && t.ms[k] < 0.95f * t.ms[2] && t.ms[k] < t.ms[best]) best = k;
+        t.chosen = t.cand[best];
+        t.phase = 4;
+    }
+    g.blocks = t.chosen;
+    return g;
+}
+
 // Caller holds h->mu.  Tier-3 launch; asynchronous on `stream`.
 int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size_t n, int32_t *d_out,
                       uint8_t *d_status, uint32_t *d_steps, uint64_t *d_stats, uint32_t budget, uint32_t flags,
@@ -3010,7 +3077,8 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
     // heavy: one thread per input, `chunk` inputs per launch (slot memory);
     // otherwise a resident grid whose threads loop over the inputs
     uint64_t chunk = n, lanes;
-    int blocks;
+    int blocks, alloc_blocks = 0;
+    GridPick tune;
     if (heavy) {
         if (nslots) {
             const uint64_t fit = h->jit_lim.slot_bytes / ((uint64_t)nslots * sizeof(int32_t));
@@ -3039,6 +3107,13 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
             if (cap < 1) return MK_ELIMIT;
             blocks = (int)std::min<uint64_t>((uint64_t)blocks, cap);
         }
+        alloc_blocks = blocks;
+        if (sorted && nslots && !sc->jit.pool && h->jit_lim.tune_grid && n >= kGridTuneMin) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone)
+                tune = grid_tune_pick(jd.tune, n, blocks);
+            blocks = tune.blocks;
+        }
         lanes = (uint64_t)blocks * block;
     }
     // stack-slot columns: one per thread, or (pool kernel) one per pool slot
@@ -3046,7 +3121,9 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
                                : sc->jit.pool      ? lanes * sc->jit.pool
                                                    : lanes;
     if (nslots) {
-        const size_t need = (size_t)nslots * slot_cols * sizeof(int32_t);
+        // (sized for the resident grid, so that a tuning launch's smaller
+        // grid does not reallocate)
+        const size_t need = (size_t)nslots * std::max<uint64_t>(slot_cols, (uint64_t)alloc_blocks * block) * sizeof(int32_t);
         if (need > sd.slots_bytes) {
             if (sd.d_slots) {
                 (void)hipDeviceSynchronize();
@@ -3119,9 +3196,11 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
             blocks = (int)std::max<uint64_t>(1, (q.n + block - 1) / block);
         }
         void *args[] = {(void *)&q};
+        if (tune.timed >= 0 && hipEventRecord(jd.tune.ev[2 * tune.timed], stream) != hipSuccess) return MK_EDEVICE;
         if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) !=
             hipSuccess)
             return MK_EDEVICE;
+        if (tune.timed >= 0 && hipEventRecord(jd.tune.ev[2 * tune.timed + 1], stream) != hipSuccess) return MK_EDEVICE;
     } while (heavy && chunk && (s0 += chunk) < n);
     return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
@@ -4223,6 +4302,11 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
                 if (wcu % 4 == 0) snprintf(w, sizeof w, "%d", wcu / 4);
                 else snprintf(w, sizeof w, "%.2f", wcu / 4.0);
                 s += std::string(" waves_per_simd=") + w;
+                // GridTune's choice for the last tuned batch size (blocks of
+                // the resident grid's), once measured
+                const mk::GridTune &t = sc->jit.dev[d].tune;
+                if (t.phase == 4 && t.cand[2])
+                    s += " grid_tuned=" + std::to_string(t.chosen) + "/" + std::to_string(t.cand[2]);
                 break;
             }
     } else {

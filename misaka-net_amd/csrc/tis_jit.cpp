@@ -2439,6 +2439,7 @@ JitLimits JitLimits::from_env()
     if (l.sat_block != 4 && l.sat_block != 8 && l.sat_block != 16 && l.sat_block != 32) l.sat_block = 4;
     num("MK_JIT_VGPR_FILE", l.vgpr_file);
     flag("MK_JIT_PAIR", l.pair);
+    flag("MK_JIT_TUNE_GRID", l.tune_grid);
     if (!l.vgpr_file || l.vgpr_file > 512) l.vgpr_file = 512;
     flag("MK_JIT_SWEEP", l.sweep);
     flag("MK_JIT_SAT_COUNT", l.sat_count);
@@ -2465,6 +2466,7 @@ std::string JitLimits::key() const
     if (prof) k += ",prof=1";
     if (vgpr_file != 512) k += ",vfile=" + std::to_string(vgpr_file);
     if (!pair) k += ",pair=0";
+    if (!tune_grid) k += ",tgrid=0";
     return k;
 }
 

@@ -134,6 +134,10 @@ struct JitLimits {
     // stack slots: one sweep pass for two sorted chunks (MK_PAIR in
     // kMachineSortKernel; MK_JIT_PAIR=0: one lane per thread).
     bool pair = true;
+    // The tile-sorted kernel's grid, for networks with stack slots in HBM
+    // and batches of 2^18 inputs or more, measured over the first launches
+    // (mk_exec.hip GridTune; MK_JIT_TUNE_GRID=0: the resident grid).
+    bool tune_grid = true;
     // Heavy stream networks whose LDS slots allow fewer than four waves per
     // CU keep more stack entries in registers until they do (MK_JIT_TUNE_REGS,
     // mk_exec.hip tune_soft_regs).

@@ -2,6 +2,7 @@
 out/status/steps on seeded inputs, plus size-independent properties at the
 BASELINE.json sizes."""
 import os
+import re
 import threading
 
 import numpy as np
@@ -272,6 +273,26 @@ def test_dynamic_stack_census_full_size(gpu, cls, mode):
     t_out, t_st, t_sp = oracle(nodes, np.arange(256, dtype=np.int64))
     assert np.array_equal(out, t_out[x]) and np.array_equal(st, t_st[x]) and np.array_equal(sp, t_sp[x])
     assert stats[0] == int(sp.astype(np.int64).sum()) and stats[2] == n
+
+
+# The tile-sorted kernel's measured grid (mk_exec.hip GridTune, round 6):
+# the first three launches at a batch size run 3/4, 1/2 and all of the
+# resident grid, a later one keeps the fastest.  Every launch of the tuning
+# sequence, and the ones after it, is exact; the plan reports the choice.
+@pytest.mark.parametrize("cls", ["data_dependent_stack_depth", "two_stacks_independent_depths"])
+def test_grid_tuning_launches_exact(gpu, cls):
+    n = (1 << 18) + 333  # a tuned size, with a partial last tile
+    nodes = mk.networks.census_classes()[cls][0][1]
+    net = mk.Network(nodes)
+    assert net.plan().startswith("tier=native") and "grid_tuned=" not in net.plan()
+    x = po.gen_inputs(SEED, n, kind=N.MK_GEN_MASKED, mask=255)
+    t_out, t_st, t_sp = oracle(nodes, np.arange(256, dtype=np.int64))
+    for k in range(6):
+        out, st, sp, stats = _device_run(net, n, gen=(N.MK_GEN_MASKED, 255))
+        assert np.array_equal(out, t_out[x]) and np.array_equal(st, t_st[x]) and np.array_equal(sp, t_sp[x]), k
+        assert stats[0] == int(sp.astype(np.int64).sum()) and stats[2] == n
+    m = re.search(r"grid_tuned=(\d+)/(\d+)", net.plan())
+    assert m and 0 < int(m.group(1)) <= int(m.group(2)), net.plan()
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -29,17 +29,23 @@ import sys
 tag, cfgs = sys.argv[1], sys.argv[2:]
 
 
-def per_dispatch(d):
+def per_dispatch(d, tuned=False):
     rows = collections.defaultdict(lambda: collections.defaultdict(float))
+    grid = {}
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
             k = r["Kernel_Name"]
             if not (k.startswith("mk_jit_exec") or "tis_" in k):
                 continue
             rows[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            grid[int(r["Dispatch_Id"])] = int(r["Grid_Size"])
+    # a kernel whose grid is measured (mk_exec.hip GridTune, grid_tuned= in
+    # the plan) runs its first launches at 3/4, 1/2 and all of the resident
+    # grid, then at the one it keeps: the launches at the grid most ran
+    keep = collections.Counter(grid[i] for i in sorted(grid)[2:]).most_common(1)
     out = {}
     for c, by in rows.items():
-        ids = sorted(by)[2:]
+        ids = [i for i in sorted(by)[2:] if not tuned or grid[i] == keep[0][0]]
         out[c] = sum(by[i] for i in ids) / max(1, len(ids))
         out[c + "_dispatches"] = len(ids)
     return out
@@ -54,11 +60,12 @@ def bench_line(path):
 
 for cfg in cfgs:
     d = os.path.join("gpurun_out", tag, cfg)
-    fetch = per_dispatch(os.path.join(d, "FETCH_SIZE"))
-    write = per_dispatch(os.path.join(d, "WRITE_SIZE"))
-    sq = per_dispatch(os.path.join(d, "SQ"))
-    lds = per_dispatch(os.path.join(d, "LDS")) if os.path.isdir(os.path.join(d, "LDS")) else {}
     rec = bench_line(os.path.join(d, "SQ.log"))
+    tuned = "grid_tuned=" in rec["config"]["executor"]
+    fetch = per_dispatch(os.path.join(d, "FETCH_SIZE"), tuned)
+    write = per_dispatch(os.path.join(d, "WRITE_SIZE"), tuned)
+    sq = per_dispatch(os.path.join(d, "SQ"), tuned)
+    lds = per_dispatch(os.path.join(d, "LDS"), tuned) if os.path.isdir(os.path.join(d, "LDS")) else {}
     workload = rec["config"]["workload"]
     lanes = rec["config"]["lanes_per_gpu"]
     retired = rec["node_instr_per_lane"] * lanes
