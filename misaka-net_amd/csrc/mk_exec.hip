@@ -1538,7 +1538,10 @@ struct JitDev {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     int per_cu = 0;
-    GridTune tune;
+    int last_blocks = 0; // grid of the last launch (a batch smaller than the resident grid, or GridTune's)
+    GridTune tune[4];    // by batch size, the oldest replaced
+    int tune_next = 0;
+    int tune_last = -1;  // entry of the last tuned launch
 };
 
 struct JitState {
@@ -1696,8 +1699,9 @@ struct mk_net {
                 (void)hipFree(sc->dev[d].d_order);
                 (void)hipFree(sc->dev[d].d_ordtab);
                 mk::release_module(sc->jit.dev[d].mod, sc->jit.rtc);
-                for (hipEvent_t e : sc->jit.dev[d].tune.ev)
-                    if (e) (void)hipEventDestroy(e);
+                for (const mk::GridTune &t : sc->jit.dev[d].tune)
+                    for (hipEvent_t e : t.ev)
+                        if (e) (void)hipEventDestroy(e);
             }
             if (c.stream) (void)hipStreamDestroy(c.stream);
             if (c.ev) (void)hipEventDestroy(c.ev);
@@ -3110,9 +3114,17 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
         alloc_blocks = blocks;
         if (sorted && nslots && !sc->jit.pool && h->jit_lim.tune_grid && n >= kGridTuneMin) {
             hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone)
-                tune = grid_tune_pick(jd.tune, n, blocks);
-            blocks = tune.blocks;
+            if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+                int e = 0;
+                while (e < 4 && jd.tune[e].n != n) e++;
+                if (e == 4) {
+                    e = jd.tune_next;
+                    jd.tune_next = (jd.tune_next + 1) % 4;
+                }
+                jd.tune_last = e;
+                tune = grid_tune_pick(jd.tune[e], n, blocks);
+                blocks = tune.blocks;
+            }
         }
         lanes = (uint64_t)blocks * block;
     }
@@ -3196,11 +3208,14 @@ int launch_jit_locked(mk_net *h, SchedCache *sc, int d, const mk_input *in, size
             blocks = (int)std::max<uint64_t>(1, (q.n + block - 1) / block);
         }
         void *args[] = {(void *)&q};
-        if (tune.timed >= 0 && hipEventRecord(jd.tune.ev[2 * tune.timed], stream) != hipSuccess) return MK_EDEVICE;
+        jd.last_blocks = blocks;
+        if (tune.timed >= 0 && hipEventRecord(jd.tune[jd.tune_last].ev[2 * tune.timed], stream) != hipSuccess)
+            return MK_EDEVICE;
         if (hipModuleLaunchKernel(jd.fn, blocks, 1, 1, (unsigned)block, 1, 1, 0, stream, args, nullptr) !=
             hipSuccess)
             return MK_EDEVICE;
-        if (tune.timed >= 0 && hipEventRecord(jd.tune.ev[2 * tune.timed + 1], stream) != hipSuccess) return MK_EDEVICE;
+        if (tune.timed >= 0 && hipEventRecord(jd.tune[jd.tune_last].ev[2 * tune.timed + 1], stream) != hipSuccess)
+            return MK_EDEVICE;
     } while (heavy && chunk && (s0 += chunk) < n);
     return fold_now(d_stats, flags) ? launch_stats_reduce(c, d_stats, stream) : MK_OK;
 }
@@ -4297,15 +4312,22 @@ int mk_net_plan(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         // evenly: 15 blocks of one wave are 3.75 per SIMD, not 3)
         for (int d = 0; d < mk::kMaxDevices; d++)
             if (sc->jit.dev[d].fn) {
-                const int wcu = sc->jit.dev[d].per_cu * sc->jit.block / 64; // waves per CU
+                // (the last launch's grid when it held fewer blocks than the
+                // resident grid: a small batch, or GridTune's choice)
+                const mk::JitDev &jd = sc->jit.dev[d];
+                const int cus = std::max(h->dev[d].cus, 1);
+                const double bcu = jd.last_blocks > 0 && jd.last_blocks < jd.per_cu * cus
+                                       ? (double)jd.last_blocks / cus : (double)jd.per_cu;
+                const double wps = bcu * sc->jit.block / 64 / 4; // waves per SIMD
                 char w[32];
-                if (wcu % 4 == 0) snprintf(w, sizeof w, "%d", wcu / 4);
-                else snprintf(w, sizeof w, "%.2f", wcu / 4.0);
+                if (wps == (double)(int)wps) snprintf(w, sizeof w, "%d", (int)wps);
+                else snprintf(w, sizeof w, "%.2f", wps);
                 s += std::string(" waves_per_simd=") + w;
                 // GridTune's choice for the last tuned batch size (blocks of
                 // the resident grid's), once measured
-                const mk::GridTune &t = sc->jit.dev[d].tune;
-                if (t.phase == 4 && t.cand[2])
+                const int tl = jd.tune_last;
+                const mk::GridTune &t = jd.tune[tl < 0 ? 0 : tl];
+                if (tl >= 0 && t.phase == 4 && t.cand[2])
                     s += " grid_tuned=" + std::to_string(t.chosen) + "/" + std::to_string(t.cand[2]);
                 break;
             }
