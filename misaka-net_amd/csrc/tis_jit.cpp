@@ -2136,12 +2136,14 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 // conflict-free (the strided layout; R consecutive inputs per thread made it
 // 4-way).
 static const char *const kMachineSortKernel = R"(
+extern "C" __device__ uint32_t __ockl_wfscan_add_u32(uint32_t, bool);
 #define MK_TS_T (256u * MK_TS_R)
 #define MK_TS_NB 256u
 extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 {
     __shared__ uint64_t s_kp[MK_TS_T]; // the tile in sorted order: position << 32 | input
-    __shared__ uint32_t s_cnt[MK_TS_NB];
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[MK_TS_NB]; // bucket counts
+    __shared__ __attribute__((aligned(16))) uint32_t s_cur[MK_TS_NB]; // bucket cursors (ranks)
     __shared__ uint32_t s_red[8];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint64_t gid = (uint64_t)blockIdx.x * 256u + tid;
@@ -2206,26 +2208,30 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             if (tid + 256u * k < m) atomicAdd(&s_cnt[bk[k]], 1u);
         }
         __syncthreads();
-        // exclusive prefix sum over the 256 buckets (thread tid owns bucket tid)
+        // the buckets' cursors, an exclusive prefix sum of the counts: every
+        // wave scans all 256 (four per lane, one DPP wave scan) and writes
+        // its own quarter's cursors to s_cur (round 6: one barrier and the
+        // per-wave totals' LDS round trip fewer; the counts stay in s_cnt
+        // for the waves still reading them)
         {
-            const uint32_t c = s_cnt[tid];
-            uint32_t x = c;
-            for (uint32_t o = 1u; o < 64u; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-                if (lane >= o) x += y;
+            const uint4 c4 = ((const uint4 *)s_cnt)[lane]; // buckets 4 lane .. 4 lane + 3
+            const uint32_t ex = __ockl_wfscan_add_u32(c4.x + c4.y + c4.z + c4.w, false);
+            if ((lane >> 4) == wave) {
+                uint4 o;
+                o.x = ex;
+                o.y = o.x + c4.x;
+                o.z = o.y + c4.y;
+                o.w = o.z + c4.z;
+                ((uint4 *)s_cur)[lane] = o;
             }
-            if (lane == 63u) s_red[wave] = x;
-            __syncthreads();
-            uint32_t pre = 0u;
-            for (uint32_t w = 0; w < wave; ++w) pre += s_red[w];
-            s_cnt[tid] = pre + x - c;
             __syncthreads();
         }
-        for (uint32_t k = 0; k < MK_TS_R; ++k) {
-            if (tid + 256u * k >= m) continue;
-            const uint32_t d = atomicAdd(&s_cnt[bk[k]], 1u);
-            s_kp[d] = (uint64_t)(tid + 256u * k) << 32 | (uint32_t)v[k];
-        }
+        // every rank first, then the scatter: the atomics' round trips overlap
+        uint32_t d[MK_TS_R];
+        for (uint32_t k = 0; k < MK_TS_R; ++k)
+            d[k] = tid + 256u * k < m ? atomicAdd(&s_cur[bk[k]], 1u) : 0u;
+        for (uint32_t k = 0; k < MK_TS_R; ++k)
+            if (tid + 256u * k < m) s_kp[d[k]] = (uint64_t)(tid + 256u * k) << 32 | (uint32_t)v[k];
         __syncthreads();
 #if MK_PROF
         pf_sort += MK_T() - pf_a;
@@ -2254,10 +2260,12 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 #if defined(MK_SWEEP_LIST)
 #define MK_SWEEP_STEP(v, loop)                                                                   \
             if (__ballot(A.sb == (v) || B.sb == (v))) {                                              \
-                const uint32_t smA_ = (loop) ? MK_WAVE_MAX(A.sb == (v) ? A.steps : 0u) : 0u;         \
-                if (A.sb == (v)) mk_run((v), A, p.budget, slots, p.lanes, pol, smA_);                \
-                const uint32_t smB_ = (loop) ? MK_WAVE_MAX(B.sb == (v) ? B.steps : 0u) : 0u;         \
-                if (B.sb == (v)) mk_run((v), B, p.budget, slots, p.lanes, pol, smB_);                \
+                /* one wave maximum for both lanes (an upper bound for each: */                      \
+                /* a loop's fast phase is only shortened by it) */                                   \
+                const uint32_t sa_ = A.sb == (v) ? A.steps : 0u, sb_ = B.sb == (v) ? B.steps : 0u;   \
+                const uint32_t sm_ = (loop) ? MK_WAVE_MAX(sa_ > sb_ ? sa_ : sb_) : 0u;               \
+                if (A.sb == (v)) mk_run((v), A, p.budget, slots, p.lanes, pol, sm_);                 \
+                if (B.sb == (v)) mk_run((v), B, p.budget, slots, p.lanes, pol, sm_);                 \
             }
             MK_SWEEP_LIST(MK_SWEEP_STEP)
 #if defined(MK_SWEEP_COLD)
