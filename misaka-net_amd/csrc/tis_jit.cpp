@@ -2208,22 +2208,20 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             if (tid + 256u * k < m) atomicAdd(&s_cnt[bk[k]], 1u);
         }
         __syncthreads();
-        // the buckets' cursors, an exclusive prefix sum of the counts: every
-        // wave scans all 256 (four per lane, one DPP wave scan) and writes
-        // its own quarter's cursors to s_cur (round 6: one barrier and the
-        // per-wave totals' LDS round trip fewer; the counts stay in s_cnt
-        // for the waves still reading them)
+        // the buckets' cursors, an exclusive prefix sum of the counts (thread
+        // tid owns bucket tid): a DPP wave scan (round 6; six __shfl_up steps
+        // were six LDS permute round trips) and the waves' totals.  Every
+        // wave scanning all 256 counts instead (one barrier fewer) measured
+        // level on C5 but 12% slower on the JRO-heavy census class
+        // (profiles/r08_c5_sort_ab.txt, r08al)
         {
-            const uint4 c4 = ((const uint4 *)s_cnt)[lane]; // buckets 4 lane .. 4 lane + 3
-            const uint32_t ex = __ockl_wfscan_add_u32(c4.x + c4.y + c4.z + c4.w, false);
-            if ((lane >> 4) == wave) {
-                uint4 o;
-                o.x = ex;
-                o.y = o.x + c4.x;
-                o.z = o.y + c4.y;
-                o.w = o.z + c4.z;
-                ((uint4 *)s_cur)[lane] = o;
-            }
+            const uint32_t c = s_cnt[tid];
+            const uint32_t x = __ockl_wfscan_add_u32(c, true);
+            if (lane == 63u) s_red[wave] = x;
+            __syncthreads();
+            uint32_t pre = 0u;
+            for (uint32_t w = 0; w < wave; ++w) pre += s_red[w];
+            s_cur[tid] = pre + x - c;
             __syncthreads();
         }
         // every rank first, then the scatter: the atomics' round trips overlap
