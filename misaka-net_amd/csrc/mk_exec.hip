@@ -2924,6 +2924,8 @@ bool jit_compile(SchedCache *sc, const JitLimits &lim)
         bool ok = jit_lane_source(sc->prog, L, lane, J.why, &J.shape, &J.max_steps, &J.heavy, false, &J.pool);
         std::string src;
         if (ok) {
+            // machine modules: the tile the launch sizes its grid by (MK_TS_R)
+            if (J.shape == JIT_MACHINE) L.ts_rounds = jit_sort_rounds(L, sc->prog.nslots);
             J.heavy = J.heavy && J.shape == JIT_STREAM;
             J.lds = jit_slots_in_lds(sc->prog.nslots, J.heavy, L);
             J.lds_n = J.heavy ? jit_lds_slot_count(sc->prog.nslots, J.heavy, L) : 0u;
@@ -4377,9 +4379,11 @@ int mk_net_jit_source(mk_net *h, const mk_opts *opts, char *out, size_t out_len)
         mk::JitLimits L = h->jit_lim; // as jit_compile: the network's LDS budget
         if (sc->lds_set) L.lds_slot_bytes = sc->lds_bytes;
         if (sc->max_dops) L.max_dops = std::max(L.max_dops, sc->max_dops);
-        if (mk::jit_lane_source(sc->prog, L, lane, why, &shape, nullptr, &heavy, false, &pool))
+        if (mk::jit_lane_source(sc->prog, L, lane, why, &shape, nullptr, &heavy, false, &pool)) {
+            if (shape == mk::JIT_MACHINE) L.ts_rounds = mk::jit_sort_rounds(L, sc->prog.nslots);
             return mk::copy_out(out, out_len, mk::jit_module_source(lane, shape, heavy && shape == mk::JIT_STREAM,
                                                                     L, pool));
+        }
     }
     (void)mk::copy_out(out, out_len, why);
     return MK_ELIMIT;

@@ -2452,7 +2452,10 @@ JitLimits JitLimits::from_env()
     flag("MK_JIT_TUNE_REGS", l.tune_regs);
     num("MK_JIT_LDS_SPLIT", l.lds_split);
     flag("MK_JIT_PROF", l.prof);
-    if (l.ts_rounds != 0 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16) l.ts_rounds = 0;
+    if (l.ts_rounds != 0 && l.ts_rounds != 1 && l.ts_rounds != 2 && l.ts_rounds != 4 && l.ts_rounds != 8 && l.ts_rounds != 16)
+        l.ts_rounds = 0;
+    num("MK_JIT_TS_ROUNDS_SLOTS", l.ts_rounds_slots);
+    if (l.ts_rounds_slots > 16 || (l.ts_rounds_slots & (l.ts_rounds_slots - 1))) l.ts_rounds_slots = 2;
     return l;
 }
 
@@ -2473,6 +2476,7 @@ std::string JitLimits::key() const
     if (vgpr_file != 512) k += ",vfile=" + std::to_string(vgpr_file);
     if (!pair) k += ",pair=0";
     if (!tune_grid) k += ",tgrid=0";
+    if (ts_rounds_slots != 2) k += ",tsrs=" + std::to_string(ts_rounds_slots);
     return k;
 }
 

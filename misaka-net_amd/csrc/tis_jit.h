@@ -104,6 +104,12 @@ struct JitLimits {
     // lanes without stack slots, 4 with them -- r02ak: C5 212-214 vs 215 us
     // but the JRO-heavy census class 58.9 vs 52.1 ms, so not the default.
     uint32_t ts_rounds = 4;
+    // ... for lanes with stack slots (MK_JIT_TS_ROUNDS_SLOTS = 1, 2, 4, 8 or
+    // 16; 0: as ts_rounds).  Round 6: tiles of 512 take the dynamic-stack
+    // census classes to more waves per SIMD (2,048 tiles fill the resident
+    // grid): t1_two_stacks 194 -> 182 us, t2_dyn_depth 119 -> 116 us; 256
+    // loses (216 / 133 us) (profiles/r08_grid_tune_ab.txt, r08ap).
+    uint32_t ts_rounds_slots = 2;
     // kMachineSortKernel dispatches by sweeps over the variants in reverse
     // postorder (tis_jit.cpp forward_order), each variant one ballot when no
     // lane is on it, instead of one variant per round (MK_JIT_SWEEP=0: rounds;
@@ -199,9 +205,12 @@ std::string jit_module_source(const std::string &lane_src, JitShape shape, bool 
                               uint32_t pool = 0);
 
 // Lanes per thread per tile of the tile-sorted machine kernel (MK_TS_R):
-// JitLimits::ts_rounds, or by the lane's stack slots when that is 0.
+// JitLimits::ts_rounds_slots for lanes with stack slots, else ts_rounds, or
+// by the lane's stack slots when that is 0.  jit_compile compiles the module
+// with it (the prelude's MK_TS_R), launch_jit_locked sizes the grid by it.
 inline uint32_t jit_sort_rounds(const JitLimits &lim, uint32_t nslots)
 {
+    if (nslots && lim.ts_rounds_slots) return lim.ts_rounds_slots;
     return lim.ts_rounds ? lim.ts_rounds : nslots ? 4u : 8u;
 }
 
