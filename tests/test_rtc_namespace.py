@@ -181,10 +181,13 @@ t = time.time()
 small = mk.Network(mk.networks.example_network()).plan()
 print("RESULT", big.split()[0], small.split()[0], round(time.time() - t, 2), flush=True)
 """
-    e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_COMPILE_S="1", AMD_COMGR_CACHE="0", MK_JIT_TUNE_REGS="0")
+    # bound 2.5 s: D = 256 compiles in ~4.4 s (round 6), past it; the small
+    # network alone in ~0.9 s, whose margin under a 1 s bound was too thin
+    # with the big compile running beside it
+    e = dict(os.environ, MK_HIPRTC=mode, MK_JIT_COMPILE_S="2.5", AMD_COMGR_CACHE="0", MK_JIT_TUNE_REGS="0")
     r = subprocess.run([sys.executable, "-c", code.format(root=ROOT)], capture_output=True, text=True, timeout=600,
                        env=e)
     assert r.returncode == 0, r.stderr[-3000:]
     _, big, small, secs = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1].split()
-    assert big == "tier=compiled", big  # D = 256 takes hiprtc ~3.7 s (round 5): past the 1 s bound
-    assert small == "tier=native" and float(secs) < 2.0, (small, secs)
+    assert big == "tier=compiled", big  # D = 256 takes hiprtc ~4.4 s: past the 2.5 s bound
+    assert small == "tier=native" and float(secs) < 3.5, (small, secs)
