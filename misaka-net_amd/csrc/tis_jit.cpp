@@ -1444,10 +1444,24 @@ void emit_self_loop(const OpWriter &w, const Graph &g, uint32_t v, size_t gpc, s
         e.line("    }");
     }
     phase(LOOP_WIDE, "T");
-    if (ind >= 0)
-        e.line("    L.steps = s0 + %uu * (uint32_t)((int64_t)((uint64_t)L.r%d - (uint64_t)i0) / (int64_t)%lld);",
-               X.inc, ind, (long long)step);
-    else
+    if (ind >= 0) {
+        // iterations = (r - i0) / step, an exact quotient below 2^32 (steps
+        // are 32-bit): |r - i0| >> ctz(step) times the inverse of step's odd
+        // part mod 2^32 -- one 32-bit multiply instead of a signed 64-bit
+        // division (round 6)
+        const uint64_t ad = step < 0 ? (uint64_t)(-step) : (uint64_t)step;
+        const int sh = __builtin_ctzll(ad);
+        const uint32_t odd = (uint32_t)(ad >> sh);
+        uint32_t inv = odd; // Newton: each step doubles the correct low bits (3 -> 6 -> 12 -> 24 -> 48)
+        for (int k = 0; k < 4; ++k) inv *= 2u - odd * inv;
+        const char *y = step < 0 ? "((uint64_t)i0 - (uint64_t)L.r%d)" : "((uint64_t)L.r%d - (uint64_t)i0)";
+        std::string ys(64, '\0');
+        ys.resize((size_t)std::snprintf(&ys[0], ys.size(), y, ind));
+        if (odd == 1u)
+            e.line("    L.steps = s0 + %uu * (uint32_t)(%s >> %d);", X.inc, ys.c_str(), sh);
+        else
+            e.line("    L.steps = s0 + %uu * ((uint32_t)(%s >> %d) * %uu);", X.inc, ys.c_str(), sh, inv);
+    } else
         e.line("    L.steps = s0 + %uu * k;", X.inc);
     e.line("    }");
     e.line("    if (more) {");
