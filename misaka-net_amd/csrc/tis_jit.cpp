@@ -2151,6 +2151,19 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
 // 4-way).
 static const char *const kMachineSortKernel = R"(
 extern "C" __device__ uint32_t __ockl_wfscan_add_u32(uint32_t, bool);
+// a chunk's end reasons: the lanes that ended, those quiescent, and the
+// three other reasons only when some lane ended otherwise (round 6)
+#define MK_TS_COUNT_REASONS(live, rs)                                                            \
+    do {                                                                                         \
+        const unsigned long long lv_ = __ballot(live), qu_ = __ballot((rs) == MK_ST_QUIESCENT);  \
+        c_done += (uint32_t)__popcll(lv_);                                                       \
+        c_qu += (uint32_t)__popcll(qu_);                                                         \
+        if (lv_ & ~qu_) {                                                                        \
+            c_bu += (uint32_t)__popcll(__ballot((rs) == MK_ST_BUDGET));                          \
+            c_ov += (uint32_t)__popcll(__ballot((rs) == MK_ST_STACK_OVERFLOW));                  \
+            c_os += (uint32_t)__popcll(__ballot((rs) == MK_ST_OUTPUT_STOP));                     \
+        }                                                                                        \
+    } while (0)
 #define MK_TS_T (256u * MK_TS_R)
 #define MK_TS_NB 256u
 extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
@@ -2309,11 +2322,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
                 const uint32_t rs = live ? (A.st & MK_ST_REASON_MASK) : 0u;
                 c_steps += live ? (uint64_t)A.steps : 0u;
                 c_out += (uint32_t)__popcll(__ballot(live && (A.st & MK_ST_HAS_OUTPUT)));
-                c_done += (uint32_t)__popcll(__ballot(live));
-                c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
-                c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
-                c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
-                c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
+                MK_TS_COUNT_REASONS(live, rs);
                 A = B;
                 kpA = kpB;
                 live = liveB;
@@ -2375,11 +2384,7 @@ extern "C" __global__ void __launch_bounds__(256) mk_jit_exec(SParams p)
             const uint32_t rs = live ? (L.st & MK_ST_REASON_MASK) : 0u;
             c_steps += live ? (uint64_t)L.steps : 0u;
             c_out += (uint32_t)__popcll(__ballot(live && (L.st & MK_ST_HAS_OUTPUT)));
-            c_done += (uint32_t)__popcll(__ballot(live));
-            c_qu += (uint32_t)__popcll(__ballot(rs == MK_ST_QUIESCENT));
-            c_bu += (uint32_t)__popcll(__ballot(rs == MK_ST_BUDGET));
-            c_ov += (uint32_t)__popcll(__ballot(rs == MK_ST_STACK_OVERFLOW));
-            c_os += (uint32_t)__popcll(__ballot(rs == MK_ST_OUTPUT_STOP));
+            MK_TS_COUNT_REASONS(live, rs);
         }
 #endif
 #if MK_PROF

@@ -295,6 +295,42 @@ def test_grid_tuning_launches_exact(gpu, cls):
     assert m and 0 < int(m.group(1)) <= int(m.group(2)), net.plan()
 
 
+# The tile-sorted kernel's end-reason counters (stats[2..6]): the other
+# three reasons are counted only when some lane of a chunk did not end
+# quiescent (round 6), so every reason is driven here -- budgets inside the
+# loops, stop-on-output, and stack overflows on a dynamic-stack class.
+@pytest.mark.parametrize("case", ["plain", "budget", "stop", "overflow"])
+def test_machine_reason_counters(gpu, case):
+    import torch
+
+    n = 300000
+    if case == "overflow":
+        nodes = mk.networks.census_classes()["data_dependent_stack_depth"][0][1]
+        kw, mask = {"stack_cap": 100}, 255
+    else:
+        nodes = mk.networks.countdown_network()
+        kw = {"budget": 700} if case == "budget" else {"stop_on_output": True} if case == "stop" else {}
+        mask = 1023
+    net = mk.Network(nodes)
+    assert "shape=machine" in net.plan(**({"stack_cap": kw["stack_cap"]} if "stack_cap" in kw else {}))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sp = torch.empty(n, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(N.MK_STATS_LEN, dtype=torch.int64, device="cuda")
+    net.compute_device(n, out_ptr=out.data_ptr(), status_ptr=st.data_ptr(), steps_ptr=sp.data_ptr(),
+                       stats_ptr=stats.data_ptr(), seed=SEED, gen_kind=N.MK_GEN_MASKED, gen_mask=mask,
+                       stream=torch.cuda.current_stream().cuda_stream, **kw)
+    torch.cuda.synchronize()
+    s_ = st.cpu().numpy()
+    r = s_ & N.MK_ST_REASON_MASK
+    got = stats.cpu().numpy()
+    want = [int((s_ & N.MK_ST_HAS_OUTPUT).astype(bool).sum()), n] + [int((r == k).sum()) for k in (1, 2, 3, 4)]
+    assert list(got[1:7]) == want, (case, list(got), want)
+    assert got[0] == int(sp.cpu().numpy().view(np.uint32).astype(np.int64).sum())
+    if case != "plain":
+        assert want[2 + {"budget": 1, "overflow": 2, "stop": 3}[case]] > 0, (case, want)
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_budget_and_stop_on_output(gpu, mode):
     nodes = [("a", "program", "JRO 0"), ("b", "program", "OUT 3\nJRO 0")]
